@@ -1,0 +1,138 @@
+"""Synthetic RGB-D workload for the bench and the parity tests.
+
+A 10.24 m box room with seeded spheres, ray-cast to z-depth (u16 millimetres, like the lounge
+PNGs read at `grid_fusion_demos/grid_demo1.py:80-84`) and a tiled colour texture, seen from a
+seeded smooth camera path that stays inside the room and looks across it (up = +z).
+
+Written against torch so the same code generates frames on the CPU (test fixtures) and
+directly in HBM on the GPU (bench: inputs resident before the timed region).  This module is
+input plumbing, not the hot path; nothing here is parity-critical because every parity test
+feeds the SAME generated arrays to the oracle and to the HIP path.
+
+Camera convention follows the reference: pixel u = fx*x/z + cx, v = fy*y/z + cy
+(`grid_fusion.py:183-197`), pose = 4x4 camera-to-world (`grid_fusion.py:265` inverts it).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+FX = FY = 585.0
+CX, CY = 320.0, 240.0
+W, H = 640, 480
+ROOM = 10.24  # metres; 512 voxels at 2 cm
+
+
+def intrinsics() -> np.ndarray:
+    """The lounge intrinsics (`data/camera-intrinsics.txt`), used for every config."""
+    return np.array([[FX, 0.0, CX], [0.0, FY, CY], [0.0, 0.0, 1.0]], dtype=np.float64)
+
+
+def make_spheres(seed: int = 0, n: int = 10, room: float = ROOM) -> np.ndarray:
+    """(n, 4) float64 [cx, cy, cz, r]: seeded spheres kept off the camera ring."""
+    rng = np.random.default_rng(seed)
+    out = []
+    c = room / 2
+    while len(out) < n:
+        r = rng.uniform(0.35, 1.1)
+        p = rng.uniform(1.2 + r, room - 1.2 - r, size=3)
+        # keep the camera ring (radius ~0.34*room around the centre, mid height) free
+        ring_d = abs(math.hypot(p[0] - c, p[1] - c) - 0.34 * room)
+        if ring_d < r + 0.6 and abs(p[2] - c) < r + 1.2:
+            continue
+        out.append([p[0], p[1], p[2], r])
+    return np.asarray(out, dtype=np.float64)
+
+
+def look_at(eye: np.ndarray, target: np.ndarray, up=(0.0, 0.0, 1.0)) -> np.ndarray:
+    """4x4 camera-to-world pose; camera x right, y down, z forward."""
+    f = target - eye
+    f = f / np.linalg.norm(f)
+    upv = np.asarray(up, dtype=np.float64)
+    x = np.cross(f, upv)
+    x = x / np.linalg.norm(x)
+    y = np.cross(f, x)
+    T = np.eye(4)
+    T[:3, 0], T[:3, 1], T[:3, 2], T[:3, 3] = x, y, f, eye
+    return T
+
+
+def trajectory(n_frames: int, seed: int = 0, room: float = ROOM, start: int = 0,
+               radius_frac: float = 0.34) -> np.ndarray:
+    """(n_frames, 4, 4) poses on a smooth seeded loop inside the room, looking across it.
+
+    Frame i of a longer run is the same pose whatever `n_frames` is (`start` offsets the
+    sequence), so a 10k-frame run continues the 1k-frame one.
+    """
+    rng = np.random.default_rng(seed + 7919)
+    ph = rng.uniform(0, 2 * np.pi, size=4)
+    c = room / 2
+    poses = np.empty((n_frames, 4, 4))
+    for k in range(n_frames):
+        t = (start + k) / 1000.0
+        th = 2 * np.pi * t + ph[0]
+        rad = radius_frac * room * (1.0 + 0.08 * math.sin(3 * th + ph[1]))
+        eye = np.array([c + rad * math.cos(th), c + rad * math.sin(th),
+                        c + 0.12 * room * math.sin(2 * th + ph[2])])
+        # look through the room centre, swinging +-35 degrees
+        sw = 0.6 * math.sin(5 * th + ph[3])
+        tgt = np.array([c - rad * math.cos(th + sw), c - rad * math.sin(th + sw),
+                        c + 0.05 * room * math.cos(th)])
+        poses[k] = look_at(eye, tgt)
+    return poses
+
+
+def render(poses, spheres: np.ndarray, room: float = ROOM, seed: int = 0, start: int = 0,
+           invalid_frac: float = 0.05, device="cpu", h: int = H, w: int = W):
+    """Ray-cast frames.  Returns torch tensors on `device`:
+    depth (F,H,W) uint16 millimetres (0 = invalid), rgb (F,H,W,3) uint8 (RGB order, like
+    `cv2.cvtColor(..., COLOR_BGR2RGB)` in the reference demos).
+    """
+    import torch
+
+    dev = torch.device(device)
+    P = torch.as_tensor(np.asarray(poses), dtype=torch.float64, device=dev)
+    S = torch.as_tensor(spheres, dtype=torch.float64, device=dev)
+    F = P.shape[0]
+    vv, uu = torch.meshgrid(torch.arange(h, device=dev, dtype=torch.float64),
+                            torch.arange(w, device=dev, dtype=torch.float64), indexing="ij")
+    dc = torch.stack([(uu - CX) / FX, (vv - CY) / FY, torch.ones_like(uu)], -1)  # (H,W,3), z = 1
+    depth = torch.empty((F, h, w), dtype=torch.int32, device=dev)
+    rgb = torch.empty((F, h, w, 3), dtype=torch.uint8, device=dev)
+    for f in range(F):
+        R, o = P[f, :3, :3], P[f, :3, 3]
+        d = dc @ R.T  # world directions, parameter t == camera z
+        inv = 1.0 / torch.where(d.abs() < 1e-12, torch.full_like(d, 1e-12), d)
+        t0 = (0.0 - o) * inv
+        t1 = (room - o) * inv
+        t = torch.maximum(t0, t1).min(-1).values  # camera is inside the box: nearest exit
+        for s in S:
+            oc = o - s[:3]
+            b = (d * oc).sum(-1)
+            a = (d * d).sum(-1)
+            cc = (oc * oc).sum() - s[3] * s[3]
+            disc = b * b - a * cc
+            ts = (-b - torch.sqrt(disc.clamp_min(0))) / a
+            hit = (disc > 0) & (ts > 1e-6) & (ts < t)
+            t = torch.where(hit, ts, t)
+        mm = torch.round(t * 1000.0).clamp(0, 65534).to(torch.int32)
+        g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + start + f)
+        drop = (torch.rand((h, w), generator=g) < invalid_frac).to(dev)
+        depth[f] = torch.where(drop, torch.zeros_like(mm), mm)
+        p = o + d * t[..., None]
+        cell = torch.floor(p / 0.16).to(torch.int64)
+        hsh = (cell[..., 0] * 73856093) ^ (cell[..., 1] * 19349669) ^ (cell[..., 2] * 83492791)
+        rgb[f, ..., 0] = ((hsh >> 3) & 255).to(torch.uint8)
+        rgb[f, ..., 1] = ((hsh >> 11) & 255).to(torch.uint8)
+        rgb[f, ..., 2] = ((hsh >> 19) & 255).to(torch.uint8)
+    return depth.to(torch.uint16), rgb
+
+
+def depth_metres(depth_u16: np.ndarray) -> np.ndarray:
+    """The reference demos' depth ingest (`grid_demo1.py:81-83`): u16 mm -> float64 metres,
+    65.535 (the 7-scenes invalid marker) -> 0."""
+    d = depth_u16.astype(float)
+    d /= 1000.0
+    d[d == 65.535] = 0
+    return d
