@@ -1,0 +1,165 @@
+/*
+ * tsdf_hip.h -- C-ABI of the MI355X (gfx950) TSDF fusion hot path.
+ *
+ * The drop-in boundary for DiWu9/Union-Thesis-SLAM's integrate path: the reference binds its
+ * device code from Python (PyCUDA SourceModule, grid_fusion.py:69-144, launched at :234-259);
+ * this library is bound the same way, from Python, through ctypes
+ * (union-thesis-slam_amd/tsdf_amd/_ffi.py).  Plain C types only: pointers, sizes, doubles.
+ *
+ * Conventions
+ *   - Every function returns int: 0 = ok, negative = TSDF_E_* code; tsdf_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ *   - A handle owns all of its device memory and one HIP stream on its device.  Host pointers
+ *     are borrowed for the duration of the call only and must be C-contiguous.
+ *   - Calls are synchronous (stream-synchronised before return) unless TSDF_ASYNC is passed;
+ *     then the caller synchronises with tsdf_*_sync().  One handle per host thread.
+ *   - Pointer residence is given per call by TSDF_DEVICE_PTRS: without it depth/colour are host
+ *     pointers (copied H2D by the call); with it they are device pointers already in HBM.
+ *   - Volumes are indexed like the reference: voxel (x, y, z), C-order (X, Y, Z), z fastest
+ *     (grid_fusion.py:52-55,158-168).  The state lives in HBM as 8x8x8 bricks;
+ *     the get/extract calls return C-order arrays.
+ */
+#ifndef TSDF_HIP_H
+#define TSDF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------------------------ */
+#define TSDF_OK 0
+#define TSDF_E_ARG -1       /* invalid argument (shape, kind, null pointer) */
+#define TSDF_E_HIP -2       /* a HIP runtime call failed (message has the HIP error string) */
+#define TSDF_E_NODEV -3     /* no usable gfx950 device */
+#define TSDF_E_CAPACITY -4  /* hash table / block pool full and could not grow */
+#define TSDF_E_OOM -5       /* device allocation failed */
+
+/* ---- input kinds and flags ---------------------------------------------------------------- */
+#define TSDF_DEPTH_U16_MM 0 /* uint16 millimetres: metres = (double)mm / 1000.0 (grid_demo1.py:81-82) */
+#define TSDF_DEPTH_F64_M 1  /* float64 metres, as handed to integrate() (grid_fusion.py:214) */
+#define TSDF_COLOR_RGB8 0   /* uint8 (H,W,3) RGB; folded B*65536+G*256+R (grid_fusion.py:228-232) */
+#define TSDF_COLOR_F32 1    /* float32 (H,W) already folded by the caller */
+
+#define TSDF_DEVICE_PTRS 1  /* depth/colour pointers are device pointers */
+#define TSDF_ASYNC 2        /* do not synchronise the handle's stream before returning */
+
+typedef struct tsdf_dense tsdf_dense_t;
+typedef struct tsdf_hash tsdf_hash_t;
+
+/* Cumulative counters since create/reset (or the last tsdf_*_stats call with reset != 0). */
+typedef struct {
+    int64_t frames;           /* frames integrated */
+    int64_t voxel_updates;    /* sum over frames of V_f (voxels whose tsdf/weight/colour changed) */
+    int64_t bricks_visited;   /* bricks that passed the conservative frustum/depth cull */
+    int64_t bricks_touched;   /* bricks with >= 1 updated voxel (B_f summed) */
+    int64_t blocks_allocated; /* hash: blocks newly allocated */
+    int64_t probe_steps;      /* hash: total linear-probe distance of block lookups */
+    int64_t probe_max;        /* hash: longest probe distance seen */
+    int64_t lookups;          /* hash: block lookups performed */
+    double kernel_ms;         /* integrate-kernel time from HIP events (profiling on only) */
+    int64_t kernel_launches;  /* integrate-kernel launches timed */
+} tsdf_stats_t;
+
+typedef struct {
+    int64_t capacity;         /* slots in the open-addressed block table (the "buckets") */
+    int64_t used;             /* live block keys */
+    int64_t tombstones;       /* removed keys not yet reclaimed by a rehash */
+    int64_t displaced;        /* live keys not in their home slot ("collisions") */
+    int64_t max_probe;        /* longest home-to-slot distance of a live key */
+    int64_t blocks_in_pool;   /* blocks handed out by the pool (live + free list) */
+    int64_t pool_capacity;    /* blocks the pool can hold before it must grow */
+    int64_t entries;          /* voxel entries (occupancy bits set), = count_num_hash_entries */
+} tsdf_hash_info_t;
+
+const char* tsdf_last_error(void);
+int tsdf_device_count(int* n);
+
+/* ---- dense grid: replaces TSDFVolume (grid_fusion.py:19-320) ------------------------------
+ * dims: voxels of THIS shard; index_offset: global voxel index of its (0,0,0) (slab sharding:
+ * world coordinates are always computed from the global index, so a slab is bit-identical to
+ * the same voxels of an unsharded volume).  origin = f32(vol_bnds[:,0]) (grid_fusion.py:44),
+ * trunc = 5 * voxel_size (grid_fusion.py:37). */
+int tsdf_dense_create(const int64_t dims[3], const int64_t index_offset[3], const float origin[3],
+                      double voxel_size, double trunc, int device, tsdf_dense_t** out);
+int tsdf_dense_destroy(tsdf_dense_t* h);
+int tsdf_dense_reset(tsdf_dense_t* h); /* tsdf = 1, weight = 0, colour = 0 (grid_fusion.py:52-55) */
+
+/* One frame: TSDFVolume.integrate(color_im, depth_im, cam_intr, cam_pose, obs_weight)
+ * (grid_fusion.py:214-314).  K: the 3x3 intrinsics as given (row-major float64); the kernel uses
+ * f64(f32(K)) like cam2pix (:190).  world_to_cam: np.linalg.inv(cam_pose) computed by the
+ * caller (:265), row-major 4x4 float64. */
+int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, const void* color,
+                         int color_kind, int height, int width, const double K[9],
+                         const double world_to_cam[16], double obs_weight, int flags);
+
+/* F frames back to back on the handle's stream (the bench's step).  depth/color point at F
+ * consecutive frames (frame stride = H*W elements); world_to_cam: F*16 doubles (host);
+ * obs_weight: F doubles (host) or NULL for all 1.0. */
+int tsdf_dense_integrate_batch(tsdf_dense_t* h, int n_frames, const void* depth, int depth_kind,
+                               const void* color, int color_kind, int height, int width,
+                               const double K[9], const double* world_to_cam,
+                               const double* obs_weight, int flags);
+
+/* get_volume (grid_fusion.py:316-320) plus weight: C-order (X,Y,Z) float32 host arrays of
+ * this shard; any pointer may be NULL to skip that field. */
+int tsdf_dense_get(tsdf_dense_t* h, float* tsdf, float* weight, float* color);
+int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf, const float* weight, const float* color);
+int tsdf_dense_sync(tsdf_dense_t* h);
+int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset);
+int tsdf_dense_set_profiling(tsdf_dense_t* h, int on);
+
+/* ---- voxel hash: replaces HashTable (hash_fusion.py:29-507) --------------------------------
+ * Keys are 8x8x8 voxel blocks; the home slot of block (bx,by,bz) is the reference's
+ * hash_function (hash_fusion.py:182-190) of the block coordinates, floor-mod `capacity`, in
+ * int64 (int_bits = 64, NumPy 2 / Linux) or wrapping int32 (int_bits = 32, the author's
+ * Windows run).  Open addressing, linear probe, lock-free CAS insert.  Shard s of n_shards
+ * owns the blocks whose home slot falls in [s*capacity/n, (s+1)*capacity/n). */
+int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_size,
+                     double trunc, int64_t capacity, int64_t max_blocks, int int_bits,
+                     int shard, int n_shards, int device, tsdf_hash_t** out);
+int tsdf_hash_destroy(tsdf_hash_t* h);
+int tsdf_hash_reset(tsdf_hash_t* h);
+
+/* HashTable.integrate (hash_fusion.py:103-145): same voxel set as the grid; obs_weight is
+ * ignored (always 1) exactly like the reference (hash_fusion.py:141,145). */
+int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const void* color,
+                        int color_kind, int height, int width, const double K[9],
+                        const double world_to_cam[16], int flags);
+int tsdf_hash_integrate_batch(tsdf_hash_t* h, int n_frames, const void* depth, int depth_kind,
+                              const void* color, int color_kind, int height, int width,
+                              const double K[9], const double* world_to_cam, int flags);
+
+/* Per-voxel entry API (get_hash_entry / add_hash_entry / remove, hash_fusion.py:199-393),
+ * batched: ijk is n x 3 int64 voxel indices (host).
+ *   lookup: found[i] = 1 and the voxel's (tsdf, weight, colour) if voxel i has an entry.
+ *   insert: creates the entry (block allocated if needed); if tsdf/weight/color are non-NULL
+ *           they set the voxel's values, else the voxel keeps (1, 0, 0).  slot[i] = table slot
+ *           of the block, local[i] = voxel index inside the block (the reference returns
+ *           (bucket, slot)).  Inserting an existing entry finds it (no duplicates).
+ *   remove: removed[i] = 1 if the entry existed; a block whose last entry goes is freed. */
+int tsdf_hash_lookup(tsdf_hash_t* h, const int64_t* ijk, int64_t n, float* tsdf, float* weight,
+                     float* color, uint8_t* found);
+int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float* tsdf,
+                     const float* weight, const float* color, int64_t* slot, int32_t* local);
+int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* removed);
+/* double_table_size (hash_fusion.py:414-437): rehash every live key into 2x the slots. */
+int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity);
+int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out);
+/* get_volume (hash_fusion.py:442-463): densify into C-order (X,Y,Z) host arrays; voxels
+ * without an entry get tsdf 1, weight 0, colour 0.  Any pointer may be NULL. */
+int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf, float* weight, float* color);
+int tsdf_hash_sync(tsdf_hash_t* h);
+int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
+int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);
+
+/* hash_function over n coordinate triples (host in, host out), computed on the device.  The
+ * same arithmetic as the kernels' home-slot computation. */
+int tsdf_hash_keys(const int64_t* xyz, int64_t n, int64_t table_size, int int_bits,
+                   int64_t* out, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSDF_HIP_H */

@@ -1,0 +1,226 @@
+"""Dense grid on the GPU vs the reference (golden fixtures) and the oracle -- bit-exact.
+
+Every test here calls the HIP path through the C-ABI (tsdf_amd -> libtsdf_hip.so).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, load_lounge, lounge_intrinsics
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+C1 = [[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]]
+
+
+@pytest.fixture(scope="module")
+def gf():
+    from tsdf_amd import grid_fusion
+    return grid_fusion
+
+
+def _same(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
+
+
+def _sparse(vol):
+    t, w, c = vol.get_state()
+    w = w.reshape(-1)
+    idx = np.flatnonzero(w > 0)
+    return idx, t.reshape(-1)[idx], w[idx], c.reshape(-1)[idx], (t, w, c)
+
+
+@pytest.mark.parametrize("name", ["dense_c1", "dense_c1_ow"])
+def test_lounge_c1_matches_reference_fixture(gf, name):
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    bnds = np.array(C1)
+    vol = gf.TSDFVolume(bnds, 0.04)
+    assert np.array_equal(bnds, g["bounds_after"])  # vol_bnds[:,1] rewritten like the reference
+    assert np.array_equal(vol._vol_dim, g["dims"]) and np.array_equal(vol._vol_origin, g["origin"])
+    K = lounge_intrinsics()
+    for f in range(3):
+        _, depth, rgb, pose = load_lounge(f)
+        vol.integrate(rgb, depth, K, pose, obs_weight=float(g["obs_weight"][f]))
+        idx, t, w, c, (T, W, C) = _sparse(vol)
+        assert np.array_equal(idx, g["f%d_idx" % f])
+        assert _same(t, g["f%d_tsdf" % f])
+        assert _same(w, g["f%d_weight" % f])
+        assert _same(c, g["f%d_color" % f])
+        # untouched voxels keep the initial state (grid_fusion.py:52-55)
+        assert np.count_nonzero(T.reshape(-1) != 1.0) == np.count_nonzero(g["f%d_tsdf" % f] != 1.0)
+    assert vol.stats()["voxel_updates"] == sum(int(g["f%d_nupd" % f]) for f in range(3))
+    tv, cv = vol.get_volume()
+    assert tv.shape == tuple(g["dims"]) and cv.dtype == np.float32
+
+
+def test_synthetic_fixture_and_depth_kinds(gf):
+    """u16-exact depth (sent as millimetres) and the same frames as float64 metres that are NOT
+    millimetre-exact (sent as f64) must both match the oracle bit for bit."""
+    g = np.load(os.path.join(GOLD, "synth_c1.npz"))
+    vol = gf.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.08)
+    for f in range(2):
+        d = g["depth_u16"][f].astype(float) / 1000.0
+        vol.integrate(g["rgb"][f], d, g["K"], g["poses"][f])
+        idx, t, w, c, _ = _sparse(vol)
+        assert np.array_equal(idx, g["f%d_idx" % f])
+        assert _same(t, g["f%d_tsdf" % f]) and _same(w, g["f%d_weight" % f]) and _same(c, g["f%d_color" % f])
+
+    # f64 path + float colour path, against the oracle
+    rng = np.random.default_rng(5)
+    vol2 = gf.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.08)
+    orc = O.OracleTSDFVolume(np.array([[0.0, 10.24]] * 3), 0.08)
+    for f in range(2):
+        d = g["depth_u16"][f].astype(float) / 1000.0 + rng.uniform(0, 1e-4, size=g["depth_u16"][f].shape)
+        d[g["depth_u16"][f] == 0] = 0
+        col = g["rgb"][f].astype(np.float64) + rng.uniform(0, 0.9, size=g["rgb"][f].shape)  # folded on host
+        vol2.integrate(col, d, g["K"], g["poses"][f], obs_weight=0.6)
+        orc.integrate(col, d, g["K"], g["poses"][f], obs_weight=0.6)
+    T, W, C = vol2.get_state()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+
+
+@pytest.mark.parametrize("bounds,vs", [
+    ([[-1.3, 1.1], [-0.9, 1.7], [0.3, 4.0]], 0.05),      # dims not multiples of 8
+    ([[-0.01, 0.01], [-0.01, 0.01], [2.0, 2.02]], 0.02),  # a single voxel
+    ([[-6.0, -5.0], [-6.0, -5.0], [-3.0, -2.0]], 0.05),   # entirely outside the frustum
+])
+def test_ragged_and_degenerate_volumes(gf, bounds, vs):
+    K = lounge_intrinsics()
+    vol = gf.TSDFVolume(np.array(bounds, float), vs)
+    orc = O.OracleTSDFVolume(np.array(bounds, float), vs)
+    for f in range(2):
+        _, depth, rgb, pose = load_lounge(f)
+        vol.integrate(rgb, depth, K, pose)
+        orc.integrate(rgb, depth, K, pose)
+    T, W, C = vol.get_state()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+
+
+def test_empty_and_invalid_depth_is_a_no_op(gf):
+    K = lounge_intrinsics()
+    vol = gf.TSDFVolume(np.array(C1), 0.04)
+    _, depth, rgb, pose = load_lounge(0)
+    vol.integrate(rgb, np.zeros_like(depth), K, pose)
+    # camera looking away from the volume
+    away = pose.copy()
+    away[:3, 2] *= -1
+    away[:3, 0] *= -1
+    vol.integrate(rgb, depth, K, away)
+    T, W, C = vol.get_state()
+    orc = O.OracleTSDFVolume(np.array(C1), 0.04)
+    orc.integrate(rgb, depth, K, away)
+    assert int(W.sum()) == int(orc._weight_vol_cpu.sum())
+    assert _same(T, orc._tsdf_vol_cpu)
+
+
+def test_lounge_512_frame0_digest(gf):
+    """G5 at full BASELINE size (512^3 @ 2 cm): count and digest of the reference's result."""
+    with open(os.path.join(GOLD, "lounge512_kat.json")) as fh:
+        kat = json.load(fh)
+    vol = gf.TSDFVolume(np.array(kat["bounds"]), kat["voxel_size"])
+    _, depth, rgb, pose = load_lounge(0)
+    vol.integrate(rgb, depth, lounge_intrinsics(), pose)
+    idx, t, w, c, _ = _sparse(vol)
+    assert len(idx) == kat["updated"] == 354352
+    h = hashlib.sha256()
+    for a in (idx.astype(np.int64), t, w, c):
+        h.update(np.ascontiguousarray(a).tobytes())
+    assert h.hexdigest() == kat["digest_idx_tsdf_weight_color"]
+
+
+def test_lounge_2cm_ten_frames_digest(gf):
+    with open(os.path.join(GOLD, "lounge2cm_kat.json")) as fh:
+        kat = json.load(fh)
+    vol = gf.TSDFVolume(np.array(kat["bounds"]), kat["voxel_size"])
+    K = lounge_intrinsics()
+    for f in range(10):
+        _, depth, _, pose = load_lounge(f, color=False)
+        vol.integrate(np.zeros(depth.shape + (3,), np.uint8), depth, K, pose)
+        assert vol.stats(reset=True)["voxel_updates"] == kat["frames"][f]["updated"]
+    idx, t, w, _, _ = _sparse(vol)
+    assert len(idx) == kat["unique"] == 389590
+    assert int(w.sum(dtype=np.float64)) == 3557017
+    h = hashlib.sha256()
+    for a in (idx.astype(np.int64), t, w):
+        h.update(np.ascontiguousarray(a).tobytes())
+    assert h.hexdigest() == kat["digest_idx_tsdf_weight"]
+
+
+def _synth(n, start=0, room=10.24):
+    from tsdf_amd import scene
+    poses = scene.trajectory(n, seed=0, start=start)
+    d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=start)
+    return d.numpy(), c.numpy(), poses
+
+
+def test_batch_equals_sequential_and_oracle(gf):
+    d, c, poses = _synth(4)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    bnds = np.array([[0.0, 10.24]] * 3)
+    seq = gf.TSDFVolume(bnds.copy(), 0.08)
+    bat = gf.TSDFVolume(bnds.copy(), 0.08)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
+    for f in range(4):
+        seq.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f])
+        orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f])
+    Tinv = np.linalg.inv(poses)
+    bat.integrate_batch(np.ascontiguousarray(d), np.ascontiguousarray(c), K, Tinv)
+    A, B = seq.get_state(), bat.get_state()
+    for a, b, o in zip(A, B, (orc._tsdf_vol_cpu, orc._weight_vol_cpu, orc._color_vol_cpu)):
+        assert _same(a, b) and _same(a, o)
+
+
+def test_device_resident_batch(gf):
+    """Inputs already in HBM (torch tensors), as the bench runs them."""
+    torch = pytest.importorskip("torch")
+    d, c, poses = _synth(3, start=500)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    bnds = np.array([[0.0, 10.24]] * 3)
+    vol = gf.TSDFVolume(bnds.copy(), 0.08)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
+    dd = torch.from_numpy(np.ascontiguousarray(d).view(np.int16)).cuda()  # raw u16 bits
+    cc = torch.from_numpy(c).cuda()
+    torch.cuda.synchronize()
+    vol.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, np.linalg.inv(poses), hw=d.shape[1:],
+                        device_ptrs=True)
+    for f in range(3):
+        orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f])
+    T, W, C = vol.get_state()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+
+
+def test_slab_shards_reassemble_bit_exact(gf):
+    """Slab sharding: x-slabs with a global index offset reproduce the
+    unsharded volume exactly, including a slab boundary that is not brick aligned."""
+    bnds = np.array(C1)
+    K = lounge_intrinsics()
+    full = gf.TSDFVolume(bnds.copy(), 0.04)
+    parts = [gf.TSDFVolume(bnds.copy(), 0.04, slab=s) for s in ((0, 43), (43, 96), (96, 128))]
+    for f in range(3):
+        _, depth, rgb, pose = load_lounge(f)
+        for v in [full] + parts:
+            v.integrate(rgb, depth, K, pose)
+    F = full.get_state()
+    P = [p.get_state() for p in parts]
+    for k in range(3):
+        assert _same(F[k], np.concatenate([p[k] for p in P], axis=0))
+
+
+def test_long_batch_without_host_sync_matches_oracle(gf):
+    """24 frames in one async batch (no host synchronisation between frames, as in the bench):
+    cross-kernel visibility of the brick state must hold whatever XCD a brick lands on."""
+    d, c, poses = _synth(24, start=40)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    bnds = np.array([[0.0, 10.24]] * 3)
+    vol = gf.TSDFVolume(bnds.copy(), 0.08)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
+    vol.integrate_batch(np.ascontiguousarray(d), np.ascontiguousarray(c), K, np.linalg.inv(poses), sync=False)
+    n = sum(orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f]) for f in range(24))
+    vol.sync()
+    T, W, C = vol.get_state()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+    assert vol.stats()["voxel_updates"] == n

@@ -1,0 +1,228 @@
+"""Voxel hash on the GPU vs the reference hash path (golden fixtures), the oracle, and the
+reference's own unit-test semantics (tests/hash_map_test.py, restated).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, load_lounge, lounge_intrinsics
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+C1 = [[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]]
+LOUNGE = [[-4.22106438, 3.86798203], [-2.6663104, 2.60146141], [0., 5.76272371]]
+
+
+@pytest.fixture(scope="module")
+def hf():
+    from tsdf_amd import hash_fusion
+    return hash_fusion
+
+
+def _entries(ht):
+    t, w, c = ht.get_state()
+    idx = np.flatnonzero(w.reshape(-1) > 0)
+    pos = np.stack(np.unravel_index(idx, t.shape), 1)
+    return pos, t.reshape(-1)[idx], w.reshape(-1)[idx], c.reshape(-1)[idx]
+
+
+@pytest.mark.parametrize("int_bits,map_size,max_blocks", [(64, 1000000, None), (32, 1000000, None),
+                                                          (64, 37, 16)])
+def test_lounge_c1_matches_reference_hash_path(hf, int_bits, map_size, max_blocks):
+    """hash_c1: the reference HashTable.integrate (per-voxel Python loop, f64 Voxel state).
+    The last case starts with a tiny table and pool, so integrate must grow both mid-frame
+    and re-run the skipped bricks exactly."""
+    g = np.load(os.path.join(GOLD, "hash_c1.npz"))
+    ht = hf.HashTable(np.array(C1), 0.04, map_size, int_bits=int_bits, max_blocks=max_blocks)
+    K = lounge_intrinsics()
+    for f in range(3):
+        _, depth, rgb, pose = load_lounge(f)
+        ht.integrate(rgb, depth, K, pose, obs_weight=2.0)  # ignored, like hash_fusion.py:141,145
+        pos, t, w, c = _entries(ht)
+        assert np.array_equal(pos, g["f%d_pos" % f])
+        assert np.array_equal(w.astype(np.float64), g["f%d_weight" % f])
+        assert np.array_equal(c.astype(np.float64), g["f%d_color" % f])
+        assert np.abs(t.astype(np.float64) - g["f%d_sdf" % f]).max() <= 1e-4  # f32 vs f64 state
+        assert np.abs(t.astype(np.float64) - g["f%d_sdf" % f]).max() <= 1e-6  # in practice
+        assert ht.count_num_hash_entries() == int(g["f%d_entries" % f])
+    info = ht.info()
+    assert info["used"] == len(np.unique(pos // 8, axis=0))  # one block per touched 8^3 brick
+    assert ht.get_load_factor() < 0.75
+
+
+def test_lookup_get_hash_entry_values(hf):
+    g = np.load(os.path.join(GOLD, "hash_c1.npz"))
+    ht = hf.HashTable(np.array(C1), 0.04)
+    _, depth, rgb, pose = load_lounge(0)
+    ht.integrate(rgb, depth, lounge_intrinsics(), pose)
+    pos = g["f0_pos"]
+    found, t, w, c = ht.lookup(pos)
+    assert found.all() and np.array_equal(w, g["f0_weight"].astype(np.float32))
+    assert np.array_equal(c, g["f0_color"].astype(np.float32))
+    e = ht.get_hash_entry(list(pos[123]))
+    assert e is not None and e.get_voxel().get_weight() == 1.0
+    assert ht.get_hash_entry([0, 0, 0]) is None or ht.lookup([[0, 0, 0]])[0][0]
+    found, *_ = ht.lookup([[-1, 0, 0], [10 ** 6, 0, 0]])  # outside the volume: not found
+    assert not found.any()
+
+
+def test_hash_function_kats_on_device(hf):
+    g = np.load(os.path.join(GOLD, "hash_kat.npz"))
+    ht64 = hf.HashTable(np.array([[0, 0.04]] * 3), 0.02, 10)
+    ht32 = hf.HashTable(np.array([[0, 0.04]] * 3), 0.02, 10, int_bits=32)
+    for si, n in enumerate(g["sizes"]):
+        assert np.array_equal(ht64.hash_keys(g["coords"], int(n)), g["h64"][si])
+        assert np.array_equal(ht32.hash_keys(g["coords"], int(n)), g["h32"][si])
+    demo = hf.HashTable(np.array(LOUNGE), 0.02, 100000)
+    assert [demo.hash_function(p) for p in ([333, 234, 241], [342, 234, 241], [332, 234, 242])] == [53356, 5995, 83120]
+
+
+# ---- hash_map_test.py restated (tests/hash_map_test.py:8-123) --------------------------------
+COORDS_A = [[80, 56, 0], [66, 23, 1], [64, 5, 2], [77, 87, 3], [22, 55, 4], [1, 62, 5], [54, 98, 6],
+            [17, 35, 7], [42, 86, 8], [75, 84, 9], [72, 56, 10], [68, 94, 11], [31, 18, 12], [97, 83, 13],
+            [21, 56, 14], [16, 38, 15], [80, 46, 16], [22, 64, 17], [68, 79, 18], [98, 10, 19],
+            [26, 31, 20], [83, 53, 21], [11, 7, 22], [92, 7, 23], [76, 81, 24], [89, 75, 25], [2, 71, 26],
+            [82, 10, 27], [77, 58, 28], [57, 0, 29], [80, 25, 30], [43, 92, 31], [15, 26, 32], [33, 93, 33],
+            [77, 25, 44], [82, 56, 45], [9, 44, 46], [54, 34, 47], [0, 73, 48], [81, 95, 49]]
+
+
+def test_resize_maintain_num_entries(hf):
+    from tsdf_amd.data_structures import HashEntry
+    ht = hf.HashTable(np.array(LOUNGE), 0.02, 10, False)
+    for p in COORDS_A:
+        ht.add_hash_entry(HashEntry(p, None, None))
+    n0 = ht._table_size
+    ht.double_table_size()
+    assert ht._table_size == 2 * n0
+    assert ht.count_num_hash_entries() == 40
+    for p in COORDS_A:
+        assert ht.get_hash_entry(p) is not None
+
+
+def test_add_until_full_and_remove_all(hf):
+    from tsdf_amd.data_structures import HashEntry
+    ht = hf.HashTable(np.array(LOUNGE), 0.02, 10, False)
+    for p in COORDS_A:
+        ht.hash_function(p)
+        slot, local = ht.add_hash_entry(HashEntry(p, None, None))
+        assert slot >= 0 and 0 <= local < 512
+    assert ht.count_num_hash_entries() == 40
+    for p in COORDS_A:
+        assert ht.remove_hash_entry(HashEntry(p, None, None)) == 1
+    assert ht.get_num_non_empty_buckets() == 0
+    assert ht.count_num_hash_entries() == 0
+    assert ht.remove_hash_entry(HashEntry(COORDS_A[0], None, None)) == 0
+
+
+def test_add_until_full_size_1000(hf):
+    from tsdf_amd.data_structures import HashEntry
+    rng = np.random.default_rng(0)  # the reference test is unseeded
+    ht = hf.HashTable(np.array(LOUNGE), 0.02, 1000, False)
+    pts = np.stack([rng.integers(0, 264, 4500), rng.integers(0, 264, 4500), np.arange(4500) % 289], 1)
+    pts = np.unique(pts, axis=0)
+    for p in pts[:300]:
+        ht.add_hash_entry(HashEntry(list(p), None, None))
+    ht.add_entries(pts[300:])
+    assert ht.count_num_hash_entries() == len(pts)
+    found, *_ = ht.lookup(pts)
+    assert found.all()
+
+
+def test_general_add_remove_readd(hf):
+    """hash_map_test.py:95-123 (seeded): 40k adds into n=10^4, 20k removes, the rest all
+    findable, 20k re-adds; entry counts at each step, compared with the oracle's restatement of
+    the reference's bucket table."""
+    from bucket_table import BucketTable
+    rng = np.random.default_rng(1)
+    ht = hf.HashTable(np.array(LOUNGE), 0.02, 10000, False)
+    X, Y, Z = (int(d) for d in ht._vol_dim)
+    pts = np.stack([rng.integers(0, X, 40000), rng.integers(0, Y, 40000), rng.integers(0, Z, 40000)], 1)
+    pts = np.unique(pts, axis=0)
+    rng.shuffle(pts)
+    ref = BucketTable(10000)
+    for p in pts[:2000]:
+        ref.add(p)
+    ht.add_entries(pts)
+    assert ht.count_num_hash_entries() == len(pts)
+    gone = pts[: len(pts) // 2]
+    keep = pts[len(pts) // 2:]
+    assert ht.remove_entries(gone).all()
+    assert ht.count_num_hash_entries() == len(keep)
+    assert ht.lookup(keep)[0].all() and not ht.lookup(gone)[0].any()
+    for p in pts[:1000]:
+        ref.remove(p)
+    assert ref.count_entries() == 1000 and all(ref.get(p) is not None for p in pts[1000:2000])
+    ht.add_entries(gone[:20000])
+    assert ht.count_num_hash_entries() == len(keep) + min(20000, len(gone))
+    info = ht.info()
+    assert info["used"] <= 0.75 * info["capacity"] + 1
+
+
+def test_entries_carry_values_and_densify(hf):
+    from tsdf_amd.data_structures import HashEntry, Voxel
+    ht = hf.HashTable(np.array(C1), 0.04, 100)
+    ht.add_hash_entry(HashEntry([3, 4, 5], None, Voxel(0.25, 65536 * 3 + 256 * 2 + 1, 2.0)))
+    v = ht.get_voxel([3, 4, 5])
+    assert (v.get_sdf(), v.get_weight(), v.get_color()) == (0.25, 2.0, 65536 * 3 + 256 * 2 + 1)
+    t, c = ht.get_volume()
+    assert t[3, 4, 5] == 0.25 and (t == 1).sum() == t.size - 1 and c[3, 4, 5] == 197121
+
+
+def test_bucket_range_shards_partition_the_keys(hf):
+    """Two shards (bucket-range ownership) hold disjoint block sets whose union is the
+    unsharded table's, with identical voxel values."""
+    K = lounge_intrinsics()
+    full = hf.HashTable(np.array(C1), 0.04, 1 << 16)
+    sh = [hf.HashTable(np.array(C1), 0.04, 1 << 16, shard=s, n_shards=2) for s in range(2)]
+    for f in range(2):
+        _, depth, rgb, pose = load_lounge(f)
+        for h in [full] + sh:
+            h.integrate(rgb, depth, K, pose)
+    Ft, Fw, Fc = full.get_state()
+    S = [h.get_state() for h in sh]
+    assert not ((S[0][1] > 0) & (S[1][1] > 0)).any()
+    W = np.where(S[0][1] > 0, S[0][1], S[1][1])
+    T = np.where(S[0][1] > 0, S[0][0], S[1][0])
+    C = np.where(S[0][1] > 0, S[0][2], S[1][2])
+    assert np.array_equal(W, Fw) and np.array_equal(T, Ft) and np.array_equal(C, Fc)
+    assert sh[0].info()["used"] + sh[1].info()["used"] == full.info()["used"]
+
+
+def test_hash_matches_dense_on_synthetic(hf):
+    """Grid vs hash side by side on the bench scene: same voxel set, weight and colour; tsdf
+    equal (both keep f32 state and apply the same update at obs_weight 1)."""
+    from tsdf_amd import grid_fusion, scene
+    poses = scene.trajectory(3, seed=0, start=250)
+    d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=250)
+    d, c = d.numpy(), c.numpy()
+    K = scene.intrinsics()
+    g = grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.04)
+    h = hf.HashTable(np.array([[0.0, 10.24]] * 3), 0.04, 1 << 18)
+    for f in range(3):
+        g.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f])
+        h.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f])
+    G, H = g.get_state(), h.get_state()
+    for a, b in zip(G, H):
+        assert np.array_equal(a, b)
+    assert g.stats()["voxel_updates"] == h.stats()["voxel_updates"]
+
+
+def test_hash_batch_without_host_sync_matches_dense(hf):
+    from tsdf_amd import grid_fusion, scene
+    poses = scene.trajectory(16, seed=0, start=700)
+    d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=700)
+    d, c = np.ascontiguousarray(d.numpy()), np.ascontiguousarray(c.numpy())
+    K = scene.intrinsics()
+    g = grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.08)
+    h = hf.HashTable(np.array([[0.0, 10.24]] * 3), 0.08, 1 << 16, max_blocks=1 << 12)
+    Tinv = np.linalg.inv(poses)
+    g.integrate_batch(d, c, K, Tinv, sync=False)
+    h.integrate_batch(d, c, K, Tinv, sync=False)
+    g.sync()
+    h.sync()
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+    sg, sh = g.stats(), h.stats()
+    assert sg["voxel_updates"] == sh["voxel_updates"] and sh["lookups"] >= sh["blocks_allocated"] > 0

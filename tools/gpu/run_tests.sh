@@ -1,0 +1,11 @@
+set -o pipefail
+mkdir -p gpurun_out
+rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
+if [ $rc -eq 0 ] || [ $rc -eq 1 ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+  echo "smoke rc=$?" >> gpurun_out/smoke.log
+fi
+exit $rc

@@ -1,0 +1,300 @@
+// tsdf_common.hip -- errors, device discovery, frame staging, pyramid launch, profiling and
+// the bulk hash_function entry point of the C-ABI (include/tsdf_hip.h).
+#include <cmath>
+#include <cstring>
+
+#include "tsdf_host.h"
+
+namespace tsdf {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+PyrLayout pyr_layout(int H, int W) {
+    PyrLayout l{};
+    int off = 0;
+    for (int L = 1; L <= kPyrLevels; ++L) {
+        l.w[L] = (W + (1 << L) - 1) >> L;
+        l.h[L] = (H + (1 << L) - 1) >> L;
+        l.off[L] = off;
+        off += l.w[L] * l.h[L];
+    }
+    l.total = off;
+    return l;
+}
+
+int Profiler::begin(hipStream_t s, hipEvent_t* e0) {
+    *e0 = nullptr;
+    if (!on) return TSDF_OK;
+    if (spare.empty()) {
+        hipEvent_t e;
+        TSDF_HIP(hipEventCreate(&e));
+        spare.push_back(e);
+    }
+    *e0 = spare.back();
+    spare.pop_back();
+    TSDF_HIP(hipEventRecord(*e0, s));
+    return TSDF_OK;
+}
+
+int Profiler::end(hipStream_t s, hipEvent_t e0) {
+    if (!on || !e0) return TSDF_OK;
+    if (spare.empty()) {
+        hipEvent_t e;
+        TSDF_HIP(hipEventCreate(&e));
+        spare.push_back(e);
+    }
+    hipEvent_t e1 = spare.back();
+    spare.pop_back();
+    TSDF_HIP(hipEventRecord(e1, s));
+    pending.emplace_back(e0, e1);
+    return TSDF_OK;
+}
+
+int Profiler::collect() {
+    for (auto& pr : pending) {
+        TSDF_HIP(hipEventSynchronize(pr.second));
+        float t = 0.0f;
+        TSDF_HIP(hipEventElapsedTime(&t, pr.first, pr.second));
+        ms += t;
+        ++launches;
+        spare.push_back(pr.first);
+        spare.push_back(pr.second);
+    }
+    pending.clear();
+    return TSDF_OK;
+}
+
+void Profiler::release() {
+    for (auto& pr : pending) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    for (auto e : spare) (void)hipEventDestroy(e);
+    pending.clear();
+    spare.clear();
+}
+
+__global__ void k_zero_u64(unsigned long long* p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0ull;
+}
+
+int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
+               double vs, double trunc) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_error(TSDF_E_NODEV, "no HIP device visible");
+    if (dev < 0 || dev >= ndev) return set_error(TSDF_E_ARG, "device %d out of range [0,%d)", dev, ndev);
+    device = dev;
+    TSDF_HIP(hipSetDevice(device));
+    for (int a = 0; a < 3; ++a) {
+        const int64_t o = off ? off[a] : 0;
+        if (dims[a] <= 0 || o < 0 || dims[a] + o > (1 << 24))
+            return set_error(TSDF_E_ARG, "dims/index_offset out of range on axis %d (%lld + %lld)", a,
+                             (long long)dims[a], (long long)o);
+        vol.dims[a] = (int)dims[a];
+        vol.off[a] = (int)o;
+        vol.nb[a] = (int)((dims[a] + kBrickEdge - 1) / kBrickEdge);
+        vol.origin[a] = origin[a];
+    }
+    if (!(vs > 0.0) || !(trunc > 0.0)) return set_error(TSDF_E_ARG, "voxel_size and trunc must be > 0");
+    vol.vs = vs;
+    vol.trunc = trunc;
+    vol.shard = 0;
+    vol.n_shards = 1;
+    n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];
+    if (n_bricks >= (1ll << 31)) return set_error(TSDF_E_ARG, "too many bricks");
+    TSDF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    TSDF_HIP(hipMalloc(&stats, sizeof(unsigned long long) * kNStat * kStatSpread));
+    TSDF_HIP(hipMemsetAsync(stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, stream));
+    return TSDF_OK;
+}
+
+int Base::ensure_pyr(int H, int W) {
+    if (pyr && H == pyr_H && W == pyr_W) return TSDF_OK;
+    if (pyr) {
+        TSDF_HIP(hipStreamSynchronize(stream));
+        TSDF_HIP(hipFree(pyr));
+        pyr = nullptr;
+    }
+    lay = pyr_layout(H, W);
+    TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total));
+    pyr_H = H;
+    pyr_W = W;
+    return TSDF_OK;
+}
+
+int check_frame_args(const void* depth, int dk, const void* color, int ck, int H, int W,
+                     const double* K, const double* Tinv) {
+    if (!depth || !color || !K || !Tinv) return set_error(TSDF_E_ARG, "null frame pointer");
+    if (dk != TSDF_DEPTH_U16_MM && dk != TSDF_DEPTH_F64_M) return set_error(TSDF_E_ARG, "bad depth_kind %d", dk);
+    if (ck != TSDF_COLOR_RGB8 && ck != TSDF_COLOR_F32) return set_error(TSDF_E_ARG, "bad color_kind %d", ck);
+    if (H <= 0 || W <= 0 || (long long)H * W >= (1ll << 31))
+        return set_error(TSDF_E_ARG, "bad image size %dx%d", H, W);
+    return TSDF_OK;
+}
+
+int Base::prepare_frame(Frame* fr, const void* depth, int dk, const void* color, int ck, int H,
+                        int W, const double K[9], const double Tinv[16], double ow, int flags,
+                        int frame_index) {
+    TSDF_TRY(ensure_pyr(H, W));
+    const size_t npx = (size_t)H * W;
+    const size_t dbytes = npx * (dk == TSDF_DEPTH_U16_MM ? 2 : 8);
+    const size_t cbytes = npx * (ck == TSDF_COLOR_RGB8 ? 3 : 4);
+    const char* d = (const char*)depth + dbytes * (size_t)frame_index;
+    const char* c = (const char*)color + cbytes * (size_t)frame_index;
+    if (!(flags & TSDF_DEVICE_PTRS)) {
+        if (st_depth_bytes < dbytes) {
+            TSDF_HIP(hipStreamSynchronize(stream));
+            if (st_depth) TSDF_HIP(hipFree(st_depth));
+            TSDF_HIP(hipMalloc(&st_depth, dbytes));
+            st_depth_bytes = dbytes;
+        }
+        if (st_color_bytes < cbytes) {
+            TSDF_HIP(hipStreamSynchronize(stream));
+            if (st_color) TSDF_HIP(hipFree(st_color));
+            TSDF_HIP(hipMalloc(&st_color, cbytes));
+            st_color_bytes = cbytes;
+        }
+        TSDF_HIP(hipMemcpyAsync(st_depth, d, dbytes, hipMemcpyHostToDevice, stream));
+        TSDF_HIP(hipMemcpyAsync(st_color, c, cbytes, hipMemcpyHostToDevice, stream));
+        d = (const char*)st_depth;
+        c = (const char*)st_color;
+    }
+    for (int r = 0; r < 12; ++r) fr->T[r] = Tinv[r];
+    fr->fx = (double)(float)K[0];
+    fr->fy = (double)(float)K[4];
+    fr->cx = (double)(float)K[2];
+    fr->cy = (double)(float)K[5];
+    fr->ow = ow;
+    fr->ow32 = (float)ow;
+    fr->H = H;
+    fr->W = W;
+    fr->depth = d;
+    fr->color = c;
+    fr->pyr = pyr;
+    for (int L = 0; L <= kPyrLevels; ++L) {
+        fr->pyr_off[L] = lay.off[L];
+        fr->pyr_w[L] = lay.w[L];
+        fr->pyr_h[L] = lay.h[L];
+    }
+    return TSDF_OK;
+}
+
+int Base::launch_pyramid(const Frame& fr, int dk) {
+    dim3 grid((fr.W + 63) / 64, (fr.H + 63) / 64);
+    if (dk == TSDF_DEPTH_U16_MM)
+        hipLaunchKernelGGL(k_pyramid<0>, grid, dim3(kWG), 0, stream, fr, pyr);
+    else
+        hipLaunchKernelGGL(k_pyramid<1>, grid, dim3(kWG), 0, stream, fr, pyr);
+    TSDF_HIP(hipGetLastError());
+    return TSDF_OK;
+}
+
+int Base::read_stats(tsdf_stats_t* out, int reset) {
+    if (!out) return set_error(TSDF_E_ARG, "null stats pointer");
+    std::vector<unsigned long long> h(kNStat * kStatSpread);
+    TSDF_HIP(hipMemcpyAsync(h.data(), stats, sizeof(unsigned long long) * h.size(),
+                            hipMemcpyDeviceToHost, stream));
+    TSDF_HIP(hipStreamSynchronize(stream));
+    TSDF_TRY(prof.collect());
+    unsigned long long s[kNStat] = {0};
+    for (int k = 0; k < kNStat; ++k)
+        for (int j = 0; j < kStatSpread; ++j) {
+            const unsigned long long x = h[k * kStatSpread + j];
+            if (k == ST_PROBE_MAX) s[k] = x > s[k] ? x : s[k];
+            else s[k] += x;
+        }
+    std::memset(out, 0, sizeof(*out));
+    out->frames = frames;
+    out->voxel_updates = (int64_t)s[ST_VOXELS];
+    out->bricks_visited = (int64_t)s[ST_VISITED];
+    out->bricks_touched = (int64_t)s[ST_TOUCHED];
+    out->blocks_allocated = (int64_t)s[ST_ALLOC];
+    out->probe_steps = (int64_t)s[ST_PROBE];
+    out->probe_max = (int64_t)s[ST_PROBE_MAX];
+    out->lookups = (int64_t)s[ST_LOOKUPS];
+    out->kernel_ms = prof.ms;
+    out->kernel_launches = prof.launches;
+    if (reset) {
+        TSDF_HIP(hipMemsetAsync(stats, 0, sizeof(unsigned long long) * h.size(), stream));
+        TSDF_HIP(hipStreamSynchronize(stream));
+        frames = 0;
+        prof.ms = 0.0;
+        prof.launches = 0;
+    }
+    return TSDF_OK;
+}
+
+int Base::set_profiling(int on) {
+    TSDF_TRY(prof.collect());
+    prof.on = on != 0;
+    return TSDF_OK;
+}
+
+void Base::release() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    prof.release();
+    if (pyr) (void)hipFree(pyr);
+    if (stats) (void)hipFree(stats);
+    if (st_depth) (void)hipFree(st_depth);
+    if (st_color) (void)hipFree(st_color);
+    if (stream) (void)hipStreamDestroy(stream);
+    pyr = nullptr;
+    stats = nullptr;
+    st_depth = st_color = nullptr;
+    stream = nullptr;
+}
+
+__global__ void k_hash_keys(const long long* xyz, long long n, long long m, int bits, long long* out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = ref_hash(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], m, bits);
+}
+
+}  // namespace tsdf
+
+using namespace tsdf;
+
+extern "C" {
+
+const char* tsdf_last_error(void) { return g_err.c_str(); }
+
+int tsdf_device_count(int* n) {
+    if (!n) return set_error(TSDF_E_ARG, "null pointer");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return TSDF_OK;
+}
+
+int tsdf_hash_keys(const int64_t* xyz, int64_t n, int64_t table_size, int int_bits, int64_t* out,
+                   int device) {
+    if (n < 0 || (n > 0 && (!xyz || !out)) || table_size <= 0 || (int_bits != 32 && int_bits != 64))
+        return set_error(TSDF_E_ARG, "tsdf_hash_keys: bad arguments");
+    if (n == 0) return TSDF_OK;
+    TSDF_HIP(hipSetDevice(device));
+    long long *dx = nullptr, *dout = nullptr;
+    TSDF_HIP(hipMalloc(&dx, sizeof(long long) * 3 * n));
+    TSDF_HIP(hipMalloc(&dout, sizeof(long long) * n));
+    TSDF_HIP(hipMemcpy(dx, xyz, sizeof(long long) * 3 * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_hash_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr,
+                       (const long long*)dx, (long long)n, (long long)table_size, int_bits, dout);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(long long) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    (void)hipFree(dout);
+    TSDF_HIP(e);
+    return TSDF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,204 @@
+// tsdf_dense.hip -- dense TSDF grid: the MI355X replacement of TSDFVolume
+// (grid_fusion.py:19-320).  HBM layout: three f32 SoA arrays of 512-voxel bricks, brick b =
+// (bx*nby + by)*nbz + bz, brick-local voxel z*64 + x*8 + y.
+#include <cstring>
+
+#include "tsdf_host.h"
+
+using namespace tsdf;
+
+struct tsdf_dense {
+    Base b;
+};
+
+namespace {
+
+__global__ void k_fill3(float* t, float* w, float* c, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        t[i] = 1.0f;
+        w[i] = 0.0f;
+        c[i] = 0.0f;
+    }
+}
+
+// brick layout <-> C-order (X,Y,Z) of the shard.  TO_CORDER: dst C-order, src bricks.
+template <bool TO_CORDER>
+__global__ void k_relayout(Vol v, const float* __restrict__ src, float* __restrict__ dst) {
+    const size_t n = (size_t)v.dims[0] * v.dims[1] * v.dims[2];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int z = (int)(i % v.dims[2]);
+        const size_t xy = i / v.dims[2];
+        const int y = (int)(xy % v.dims[1]);
+        const int x = (int)(xy / v.dims[1]);
+        const size_t b = ((size_t)(x >> 3) * v.nb[1] + (y >> 3)) * v.nb[2] + (z >> 3);
+        const size_t j = b * kBrickVox + (size_t)(z & 7) * 64 + (x & 7) * 8 + (y & 7);
+        if (TO_CORDER) dst[i] = src[j];
+        else dst[j] = src[i];
+    }
+}
+
+int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void* color, int ck,
+              int H, int W, const double* K, const double* Tinv, const double* ow, int flags) {
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    const Table no_table{};
+    const unsigned grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    for (int f = 0; f < n_frames; ++f) {
+        Frame fr;
+        TSDF_TRY(B.prepare_frame(&fr, depth, dk, color, ck, H, W, K, Tinv + 16 * (size_t)f,
+                                 ow ? ow[f] : 1.0, flags, f));
+        TSDF_TRY(B.launch_pyramid(fr, dk));
+        hipEvent_t e0;
+        TSDF_TRY(B.prof.begin(B.stream, &e0));
+        if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
+            hipLaunchKernelGGL((k_integrate<false, 0, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
+        else if (dk == TSDF_DEPTH_U16_MM)
+            hipLaunchKernelGGL((k_integrate<false, 0, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
+        else if (ck == TSDF_COLOR_RGB8)
+            hipLaunchKernelGGL((k_integrate<false, 1, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
+        else
+            hipLaunchKernelGGL((k_integrate<false, 1, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
+        TSDF_HIP(hipGetLastError());
+        TSDF_TRY(B.prof.end(B.stream, e0));
+        ++B.frames;
+    }
+    if (!(flags & TSDF_ASYNC)) TSDF_HIP(hipStreamSynchronize(B.stream));
+    return TSDF_OK;
+}
+
+int dense_xfer(tsdf_dense* h, float* tsdf_, float* weight_, float* color_, bool get) {
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    const size_t n = (size_t)B.vol.dims[0] * B.vol.dims[1] * B.vol.dims[2];
+    float* tmp = nullptr;
+    TSDF_HIP(hipMalloc(&tmp, n * sizeof(float)));
+    float* host[3] = {tsdf_, weight_, color_};
+    float* dev[3] = {B.pool.tsdf, B.pool.weight, B.pool.color};
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 3 && e == hipSuccess; ++k) {
+        if (!host[k]) continue;
+        if (get) {
+            hipLaunchKernelGGL(k_relayout<true>, dim3(4096), dim3(256), 0, B.stream, B.vol, (const float*)dev[k], tmp);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipMemcpyAsync(host[k], tmp, n * sizeof(float), hipMemcpyDeviceToHost, B.stream);
+        } else {
+            e = hipMemcpyAsync(tmp, host[k], n * sizeof(float), hipMemcpyHostToDevice, B.stream);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_relayout<false>, dim3(4096), dim3(256), 0, B.stream, B.vol, (const float*)tmp, dev[k]);
+                e = hipGetLastError();
+            }
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(B.stream);
+    }
+    (void)hipFree(tmp);
+    TSDF_HIP(e);
+    return TSDF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tsdf_dense_create(const int64_t dims[3], const int64_t index_offset[3], const float origin[3],
+                      double voxel_size, double trunc, int device, tsdf_dense_t** out) {
+    if (!dims || !origin || !out) return set_error(TSDF_E_ARG, "null pointer");
+    *out = nullptr;
+    tsdf_dense* h = new tsdf_dense();
+    int r = h->b.init(device, dims, index_offset, origin, voxel_size, trunc);
+    if (r == TSDF_OK) {
+        const size_t n = (size_t)h->b.n_bricks * kBrickVox * sizeof(float);
+        hipError_t e = hipMalloc(&h->b.pool.tsdf, n);
+        if (e == hipSuccess) e = hipMalloc(&h->b.pool.weight, n);
+        if (e == hipSuccess) e = hipMalloc(&h->b.pool.color, n);
+        if (e != hipSuccess)
+            r = set_error(e == hipErrorOutOfMemory ? TSDF_E_OOM : TSDF_E_HIP,
+                          "allocating %zu bytes of brick state: %s", 3 * n, hipGetErrorString(e));
+    }
+    if (r == TSDF_OK) r = tsdf_dense_reset(h);
+    if (r != TSDF_OK) {
+        std::string keep = tsdf_last_error();
+        tsdf_dense_destroy(h);
+        set_error(r, "%s", keep.c_str());
+        return r;
+    }
+    *out = h;
+    return TSDF_OK;
+}
+
+int tsdf_dense_destroy(tsdf_dense_t* h) {
+    if (!h) return TSDF_OK;
+    (void)hipSetDevice(h->b.device);
+    h->b.release();
+    if (h->b.pool.tsdf) (void)hipFree(h->b.pool.tsdf);
+    if (h->b.pool.weight) (void)hipFree(h->b.pool.weight);
+    if (h->b.pool.color) (void)hipFree(h->b.pool.color);
+    delete h;
+    return TSDF_OK;
+}
+
+int tsdf_dense_reset(tsdf_dense_t* h) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    hipLaunchKernelGGL(k_fill3, dim3(4096), dim3(256), 0, B.stream, B.pool.tsdf, B.pool.weight,
+                       B.pool.color, (size_t)B.n_bricks * kBrickVox);
+    TSDF_HIP(hipGetLastError());
+    TSDF_HIP(hipMemsetAsync(B.stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    B.frames = 0;
+    return TSDF_OK;
+}
+
+int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, const void* color,
+                         int color_kind, int height, int width, const double K[9],
+                         const double world_to_cam[16], double obs_weight, int flags) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    return dense_run(h, 1, depth, depth_kind, color, color_kind, height, width, K, world_to_cam,
+                     &obs_weight, flags);
+}
+
+int tsdf_dense_integrate_batch(tsdf_dense_t* h, int n_frames, const void* depth, int depth_kind,
+                               const void* color, int color_kind, int height, int width,
+                               const double K[9], const double* world_to_cam,
+                               const double* obs_weight, int flags) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    if (n_frames < 0) return set_error(TSDF_E_ARG, "n_frames < 0");
+    if (n_frames == 0) return TSDF_OK;
+    TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    return dense_run(h, n_frames, depth, depth_kind, color, color_kind, height, width, K,
+                     world_to_cam, obs_weight, flags);
+}
+
+int tsdf_dense_get(tsdf_dense_t* h, float* tsdf_, float* weight_, float* color_) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    return dense_xfer(h, tsdf_, weight_, color_, true);
+}
+
+int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf_, const float* weight_, const float* color_) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    return dense_xfer(h, (float*)tsdf_, (float*)weight_, (float*)color_, false);
+}
+
+int tsdf_dense_sync(tsdf_dense_t* h) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_HIP(hipStreamSynchronize(h->b.stream));
+    return TSDF_OK;
+}
+
+int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    return h->b.read_stats(out, reset);
+}
+
+int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    return h->b.set_profiling(on);
+}
+
+}  // extern "C"

@@ -1,0 +1,751 @@
+// tsdf_hash.hip -- voxel-hash map store: the MI355X replacement of HashTable
+// (hash_fusion.py:29-507).
+//
+// Keys are 8^3 voxel blocks (bx,by,bz) packed into 63 bits; the home slot is the reference's
+// hash_function of the block coordinates (hash_fusion.py:182-190).  Open addressing with
+// linear probing over `capacity` slots; keys go EMPTY -> key by CAS only, removal leaves a
+// tombstone; a resize rehashes every live key (double_table_size, hash_fusion.py:414-437).
+// Blocks come from a pool (SoA f32 bricks like the dense grid) with a bump allocator and a
+// free list.  A voxel "entry" (count_num_hash_entries, get_hash_entry) is one bit of the
+// block's 512-bit occupancy mask, set by integrate or by an explicit insert.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "tsdf_host.h"
+
+using namespace tsdf;
+
+struct tsdf_hash {
+    Base b;
+    Table t{};          // device view (pointers + capacity)
+    PoolState host_st{};
+    int* d_list = nullptr;  // re-run list
+    int list_cap = 0;
+};
+
+namespace {
+
+struct InfoDev {
+    unsigned long long used, tomb, displaced, max_probe, entries;
+};
+
+__global__ void k_fill_keys(unsigned long long* k, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        k[i] = kEmpty;
+}
+
+// After each allocating launch: fold the launch's allocations into the pool state.
+__global__ void k_commit(PoolState* st, long long max_blocks) {
+    const long long used = coh_load(&st->cursor);
+    const long long nf = coh_load(&st->free_count);
+    const long long cons = used < nf ? used : nf;
+    const long long top = coh_load(&st->pool_top) + (used - cons);
+    coh_store(&st->free_count, nf - cons);
+    coh_store(&st->pool_top, top < max_blocks ? top : max_blocks);
+    coh_store(&st->cursor, 0ll);
+}
+
+// Single-thread linear probe; returns the slot or -1.
+__device__ long long probe_find(const Table& t, unsigned long long key, long long home) {
+    long long s = home;
+    for (long long n = 0; n < t.capacity; ++n) {
+        const unsigned long long k = coh_load(&t.keys[s]);
+        if (k == key) return s;
+        if (k == kEmpty) return -1;
+        if (++s == t.capacity) s = 0;
+    }
+    return -1;
+}
+
+__device__ bool voxel_brick(const Vol& v, long long x, long long y, long long z, int* bx, int* by,
+                            int* bz, int* local) {
+    if (x < 0 || y < 0 || z < 0 || x >= v.dims[0] || y >= v.dims[1] || z >= v.dims[2]) return false;
+    *bx = (int)(x >> 3);
+    *by = (int)(y >> 3);
+    *bz = (int)(z >> 3);
+    *local = (int)((z & 7) * 64 + (x & 7) * 8 + (y & 7));
+    return true;
+}
+
+__global__ void k_lookup(Vol v, Table t, Pool pool, const long long* ijk, long long n, float* ot,
+                         float* ow, float* oc, unsigned char* found) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int bx, by, bz, local;
+    unsigned char f = 0;
+    float tv = 1.0f, wv = 0.0f, cv = 0.0f;
+    if (voxel_brick(v, ijk[3 * i], ijk[3 * i + 1], ijk[3 * i + 2], &bx, &by, &bz, &local)) {
+        const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
+        if (s >= 0) {
+            const long long blk = coh_load(&t.vals[s]);
+            const unsigned long long word = coh_load(&t.occ[blk * 8 + (local >> 6)]);
+            if ((word >> (local & 63)) & 1ull) {
+                f = 1;
+                const size_t j = (size_t)blk * kBrickVox + local;
+                tv = coh_load(&pool.tsdf[j]);
+                wv = coh_load(&pool.weight[j]);
+                cv = coh_load(&pool.color[j]);
+            }
+        }
+    }
+    found[i] = f;
+    if (ot) ot[i] = tv;
+    if (ow) ow[i] = wv;
+    if (oc) oc[i] = cv;
+}
+
+// Find-or-insert of unique block keys, one thread per key.  Keys are distinct, but two
+// threads can race for the same empty slot: the loser keeps its block and probes on.  New
+// blocks are initialised to (1, 0, 0) with empty entry masks.
+__global__ void k_insert_blocks(Table t, Pool pool, const unsigned long long* keys, long long n,
+                                int* blk_out, long long* slot_out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long key = keys[i];
+    const int bx = (int)(key & 0x1FFFFF), by = (int)((key >> 21) & 0x1FFFFF), bz = (int)(key >> 42);
+    long long s = ref_hash(bx, by, bz, t.capacity, t.int_bits);
+    long long tomb = -1;
+    int b = -1;
+    blk_out[i] = -1;
+    slot_out[i] = -1;
+    for (long long m = 0; m < 2 * t.capacity; ++m) {
+        const unsigned long long k = coh_load(&t.keys[s]);
+        if (k == key) {
+            blk_out[i] = coh_load(&t.vals[s]);
+            slot_out[i] = s;
+            return;  // (a spare block from a lost race stays unused)
+        }
+        if (k == kTomb && tomb < 0) tomb = s;
+        if (k == kEmpty) {
+            const long long target = tomb >= 0 ? tomb : s;
+            const unsigned long long expect = tomb >= 0 ? kTomb : kEmpty;
+            if (b < 0) b = pool_alloc(t);
+            if (b < 0) return;  // pool full
+            if (atomicCAS(&t.keys[target], expect, key) == expect) {
+                coh_store(&t.vals[target], b);
+                for (int k2 = 0; k2 < 8; ++k2) coh_store(&t.occ[(size_t)b * 8 + k2], 0ull);
+                for (int j = 0; j < kBrickVox; ++j) {
+                    pool.tsdf[(size_t)b * kBrickVox + j] = 1.0f;
+                    pool.weight[(size_t)b * kBrickVox + j] = 0.0f;
+                    pool.color[(size_t)b * kBrickVox + j] = 0.0f;
+                }
+                blk_out[i] = b;
+                slot_out[i] = target;
+                return;
+            }
+            // lost the slot to another key: probe on past it
+            s = target;
+            tomb = -1;
+        }
+        if (++s == t.capacity) s = 0;
+    }
+}
+
+__global__ void k_set_voxels(Vol v, Table t, Pool pool, const long long* ijk, long long n,
+                             const float* it, const float* iw, const float* ic) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int bx, by, bz, local;
+    if (!voxel_brick(v, ijk[3 * i], ijk[3 * i + 1], ijk[3 * i + 2], &bx, &by, &bz, &local)) return;
+    const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
+    if (s < 0) return;
+    const long long blk = coh_load(&t.vals[s]);
+    atomicOr(&t.occ[blk * 8 + (local >> 6)], 1ull << (local & 63));
+    const size_t j = (size_t)blk * kBrickVox + local;
+    if (it) pool.tsdf[j] = it[i];
+    if (iw) pool.weight[j] = iw[i];
+    if (ic) pool.color[j] = ic[i];
+}
+
+__global__ void k_remove_voxels(Vol v, Table t, const long long* ijk, long long n,
+                                unsigned char* removed) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int bx, by, bz, local;
+    unsigned char r = 0;
+    if (voxel_brick(v, ijk[3 * i], ijk[3 * i + 1], ijk[3 * i + 2], &bx, &by, &bz, &local)) {
+        const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
+        if (s >= 0) {
+            const long long blk = coh_load(&t.vals[s]);
+            const unsigned long long bit = 1ull << (local & 63);
+            const unsigned long long old = atomicAnd(&t.occ[blk * 8 + (local >> 6)], ~bit);
+            r = (old & bit) ? 1 : 0;
+        }
+    }
+    if (removed) removed[i] = r;
+}
+
+// Blocks whose every entry is gone are unlinked (tombstone) and returned to the free list.
+__global__ void k_free_empty(Table t, const unsigned long long* keys, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long key = keys[i];
+    const int bx = (int)(key & 0x1FFFFF), by = (int)((key >> 21) & 0x1FFFFF), bz = (int)(key >> 42);
+    const long long s = probe_find(t, key, ref_hash(bx, by, bz, t.capacity, t.int_bits));
+    if (s < 0) return;
+    const long long blk = coh_load(&t.vals[s]);
+    for (int k = 0; k < 8; ++k)
+        if (coh_load(&t.occ[blk * 8 + k])) return;
+    coh_store(&t.keys[s], kTomb);
+    const unsigned long long f = atomicAdd((unsigned long long*)&t.st->free_count, 1ull);
+    coh_store(&t.free_list[f], (int)blk);
+}
+
+__global__ void k_rehash(Table src, Table dst) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < src.capacity;
+         i += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long key = coh_load(&src.keys[i]);
+        if (key == kEmpty || key == kTomb) continue;
+        const int bx = (int)(key & 0x1FFFFF), by = (int)((key >> 21) & 0x1FFFFF), bz = (int)(key >> 42);
+        long long s = ref_hash(bx, by, bz, dst.capacity, dst.int_bits);
+        for (long long m = 0; m < dst.capacity; ++m) {
+            if (atomicCAS(&dst.keys[s], kEmpty, key) == kEmpty) {
+                coh_store(&dst.vals[s], coh_load(&src.vals[i]));
+                break;
+            }
+            if (++s == dst.capacity) s = 0;
+        }
+    }
+}
+
+__global__ void k_info(Table t, InfoDev* out) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < t.capacity;
+         i += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long key = coh_load(&t.keys[i]);
+        if (key == kEmpty) continue;
+        if (key == kTomb) {
+            atomicAdd(&out->tomb, 1ull);
+            continue;
+        }
+        atomicAdd(&out->used, 1ull);
+        const int bx = (int)(key & 0x1FFFFF), by = (int)((key >> 21) & 0x1FFFFF), bz = (int)(key >> 42);
+        const long long home = ref_hash(bx, by, bz, t.capacity, t.int_bits);
+        const long long d = (i - home + t.capacity) % t.capacity;
+        if (d) atomicAdd(&out->displaced, 1ull);
+        atomicMax(&out->max_probe, (unsigned long long)d);
+        const long long blk = coh_load(&t.vals[i]);
+        unsigned long long c = 0;
+        for (int k = 0; k < 8; ++k) c += __popcll(coh_load(&t.occ[blk * 8 + k]));
+        if (c) atomicAdd(&out->entries, c);
+    }
+}
+
+// Densify (hash_fusion.py:442-463): one thread per (slot, z-plane of the block); the 64 bits
+// of that plane's entry mask select the voxels to write.
+__global__ void k_to_dense(Vol v, Table t, Pool pool, float* ot, float* ow, float* oc) {
+    const long long total = t.capacity * kBrickEdge;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long s = i >> 3;
+        const int kz = (int)(i & 7);
+        const unsigned long long key = coh_load(&t.keys[s]);
+        if (key == kEmpty || key == kTomb) continue;
+        const long long blk = coh_load(&t.vals[s]);
+        unsigned long long m = coh_load(&t.occ[blk * 8 + kz]);
+        const int bx = (int)(key & 0x1FFFFF), by = (int)((key >> 21) & 0x1FFFFF), bz = (int)(key >> 42);
+        while (m) {
+            const int bit = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int x = bx * 8 + (bit >> 3), y = by * 8 + (bit & 7), z = bz * 8 + kz;
+            if (x >= v.dims[0] || y >= v.dims[1] || z >= v.dims[2]) continue;
+            const size_t o = ((size_t)x * v.dims[1] + y) * v.dims[2] + z;
+            const size_t j = (size_t)blk * kBrickVox + kz * 64 + bit;
+            if (ot) ot[o] = coh_load(&pool.tsdf[j]);
+            if (ow) ow[o] = coh_load(&pool.weight[j]);
+            if (oc) oc[o] = coh_load(&pool.color[j]);
+        }
+    }
+}
+
+__global__ void k_fill_dense(float* t, float* w, float* c, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        if (t) t[i] = 1.0f;
+        if (w) w[i] = 0.0f;
+        if (c) c[i] = 0.0f;
+    }
+}
+
+int read_state(tsdf_hash* h) {
+    TSDF_HIP(hipMemcpyAsync(&h->host_st, h->t.st, sizeof(PoolState), hipMemcpyDeviceToHost, h->b.stream));
+    TSDF_HIP(hipStreamSynchronize(h->b.stream));
+    return TSDF_OK;
+}
+
+int grow_pool(tsdf_hash* h, long long new_max) {
+    Base& B = h->b;
+    Table& t = h->t;
+    const size_t old_n = (size_t)t.max_blocks, nn = (size_t)new_max;
+    float* nt = nullptr;
+    float* nw = nullptr;
+    float* nc = nullptr;
+    unsigned long long* no = nullptr;
+    int* nf = nullptr;
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    TSDF_HIP(hipMalloc(&nt, nn * kBrickVox * sizeof(float)));
+    TSDF_HIP(hipMalloc(&nw, nn * kBrickVox * sizeof(float)));
+    TSDF_HIP(hipMalloc(&nc, nn * kBrickVox * sizeof(float)));
+    TSDF_HIP(hipMalloc(&no, nn * 8 * sizeof(unsigned long long)));
+    TSDF_HIP(hipMalloc(&nf, nn * sizeof(int)));
+    TSDF_HIP(hipMemcpyAsync(nt, B.pool.tsdf, old_n * kBrickVox * sizeof(float), hipMemcpyDeviceToDevice, B.stream));
+    TSDF_HIP(hipMemcpyAsync(nw, B.pool.weight, old_n * kBrickVox * sizeof(float), hipMemcpyDeviceToDevice, B.stream));
+    TSDF_HIP(hipMemcpyAsync(nc, B.pool.color, old_n * kBrickVox * sizeof(float), hipMemcpyDeviceToDevice, B.stream));
+    TSDF_HIP(hipMemcpyAsync(no, t.occ, old_n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, B.stream));
+    TSDF_HIP(hipMemcpyAsync(nf, t.free_list, old_n * sizeof(int), hipMemcpyDeviceToDevice, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    (void)hipFree(B.pool.tsdf);
+    (void)hipFree(B.pool.weight);
+    (void)hipFree(B.pool.color);
+    (void)hipFree(t.occ);
+    (void)hipFree(t.free_list);
+    B.pool.tsdf = nt;
+    B.pool.weight = nw;
+    B.pool.color = nc;
+    t.occ = no;
+    t.free_list = nf;
+    t.max_blocks = new_max;
+    return TSDF_OK;
+}
+
+int resize_table(tsdf_hash* h, long long new_cap) {
+    Base& B = h->b;
+    Table nt = h->t;
+    nt.capacity = new_cap;
+    TSDF_HIP(hipMalloc(&nt.keys, sizeof(unsigned long long) * new_cap));
+    TSDF_HIP(hipMalloc(&nt.vals, sizeof(int) * new_cap));
+    hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, nt.keys, (long long)new_cap);
+    TSDF_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_rehash, dim3(2048), dim3(256), 0, B.stream, h->t, nt);
+    TSDF_HIP(hipGetLastError());
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    (void)hipFree(h->t.keys);
+    (void)hipFree(h->t.vals);
+    h->t.keys = nt.keys;
+    h->t.vals = nt.vals;
+    h->t.capacity = new_cap;
+    return TSDF_OK;
+}
+
+int info_raw(tsdf_hash* h, InfoDev* out) {
+    Base& B = h->b;
+    InfoDev* d = nullptr;
+    TSDF_HIP(hipMalloc(&d, sizeof(InfoDev)));
+    TSDF_HIP(hipMemsetAsync(d, 0, sizeof(InfoDev), B.stream));
+    hipLaunchKernelGGL(k_info, dim3(2048), dim3(256), 0, B.stream, h->t, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(InfoDev), hipMemcpyDeviceToHost, B.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(B.stream);
+    (void)hipFree(d);
+    TSDF_HIP(e);
+    return TSDF_OK;
+}
+
+// Grow whatever ran out (reference policy: keep slots used below 0.75 of capacity, like
+// needs_resize, hash_fusion.py:156-161), then re-run the bricks that were skipped.
+int ensure_room(tsdf_hash* h) {
+    InfoDev inf{};
+    TSDF_TRY(info_raw(h, &inf));
+    TSDF_TRY(read_state(h));
+    if (h->host_st.pool_top + 64 >= h->t.max_blocks && h->host_st.free_count < 64)
+        TSDF_TRY(grow_pool(h, h->t.max_blocks * 2));
+    if ((double)(inf.used + inf.tomb) >= 0.75 * (double)h->t.capacity)
+        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+    return TSDF_OK;
+}
+
+template <bool HASH>
+void launch_integrate(tsdf_hash* h, const Frame& fr, int dk, int ck, unsigned grid, const int* list, int n_list) {
+    Base& B = h->b;
+    if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
+        hipLaunchKernelGGL((k_integrate<true, 0, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
+    else if (dk == TSDF_DEPTH_U16_MM)
+        hipLaunchKernelGGL((k_integrate<true, 0, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
+    else if (ck == TSDF_COLOR_RGB8)
+        hipLaunchKernelGGL((k_integrate<true, 1, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
+    else
+        hipLaunchKernelGGL((k_integrate<true, 1, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
+}
+
+int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int ck,
+             int H, int W, const double* K, const double* Tinv, int flags) {
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    const unsigned grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    const bool sync_each = !(flags & TSDF_ASYNC) && n_frames == 1;
+    for (int f = 0; f < n_frames; ++f) {
+        Frame fr;
+        // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
+        TSDF_TRY(B.prepare_frame(&fr, depth, dk, color, ck, H, W, K, Tinv + 16 * (size_t)f, 1.0, flags, f));
+        TSDF_TRY(B.launch_pyramid(fr, dk));
+        hipEvent_t e0;
+        TSDF_TRY(B.prof.begin(B.stream, &e0));
+        launch_integrate<true>(h, fr, dk, ck, grid, nullptr, 0);
+        TSDF_HIP(hipGetLastError());
+        TSDF_TRY(B.prof.end(B.stream, e0));
+        hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+        TSDF_HIP(hipGetLastError());
+        ++B.frames;
+        if (!sync_each) continue;
+        // Synchronous frame: recover from a full table/pool exactly (the skipped bricks were
+        // not touched), then keep the reference's load-factor policy for the next frame.
+        TSDF_TRY(read_state(h));
+        for (int round = 0; h->host_st.n_overflow > 0 && round < 40; ++round) {
+            const long long n_ov = h->host_st.n_overflow;
+            if (n_ov > h->t.overflow_cap)
+                return set_error(TSDF_E_CAPACITY, "overflow list exceeded (%lld bricks)", n_ov);
+            if (h->list_cap < n_ov) {
+                if (h->d_list) (void)hipFree(h->d_list);
+                TSDF_HIP(hipMalloc(&h->d_list, sizeof(int) * n_ov));
+                h->list_cap = (int)n_ov;
+            }
+            TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(int) * n_ov, hipMemcpyDeviceToDevice, B.stream));
+            TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
+            // grow: double the pool if it is the limit, else the table
+            InfoDev inf{};
+            TSDF_TRY(info_raw(h, &inf));
+            if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
+                TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
+            else
+                TSDF_TRY(resize_table(h, h->t.capacity * 2));
+            launch_integrate<true>(h, fr, dk, ck, (unsigned)((n_ov + kWG - 1) / kWG), h->d_list, (int)n_ov);
+            TSDF_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+            TSDF_HIP(hipGetLastError());
+            TSDF_TRY(read_state(h));
+        }
+        if (h->host_st.n_overflow > 0) return set_error(TSDF_E_CAPACITY, "could not make room in the hash table");
+        TSDF_TRY(ensure_room(h));
+    }
+    if (!(flags & TSDF_ASYNC) && !sync_each) {
+        TSDF_TRY(read_state(h));
+        if (h->host_st.n_overflow > 0)
+            return set_error(TSDF_E_CAPACITY,
+                             "batch ran out of table/pool space (%lld bricks skipped); create the table "
+                             "with more capacity/max_blocks or integrate frame by frame",
+                             (long long)h->host_st.n_overflow);
+    }
+    return TSDF_OK;
+}
+
+int upload(tsdf_hash* h, const void* src, size_t bytes, void** dst) {
+    *dst = nullptr;
+    if (!src || !bytes) return TSDF_OK;
+    TSDF_HIP(hipMalloc(dst, bytes));
+    TSDF_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, h->b.stream));
+    return TSDF_OK;
+}
+
+// unique packed block keys of the in-volume voxels of ijk
+std::vector<unsigned long long> unique_blocks(const Vol& v, const int64_t* ijk, int64_t n) {
+    std::vector<unsigned long long> keys;
+    keys.reserve((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
+        if (x < 0 || y < 0 || z < 0 || x >= v.dims[0] || y >= v.dims[1] || z >= v.dims[2]) continue;
+        keys.push_back(pack_key((int)(x >> 3), (int)(y >> 3), (int)(z >> 3)));
+    }
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    return keys;
+}
+
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() {
+        for (void* q : p)
+            if (q) (void)hipFree(q);
+    }
+    void* add(void* q) {
+        p.push_back(q);
+        return q;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_size, double trunc,
+                     int64_t capacity, int64_t max_blocks, int int_bits, int shard, int n_shards,
+                     int device, tsdf_hash_t** out) {
+    if (!dims || !origin || !out) return set_error(TSDF_E_ARG, "null pointer");
+    *out = nullptr;
+    if (capacity <= 0 || capacity > (1ll << 40)) return set_error(TSDF_E_ARG, "capacity out of range");
+    if (int_bits != 32 && int_bits != 64) return set_error(TSDF_E_ARG, "int_bits must be 32 or 64");
+    if (n_shards < 1 || shard < 0 || shard >= n_shards) return set_error(TSDF_E_ARG, "bad shard %d/%d", shard, n_shards);
+    tsdf_hash* h = new tsdf_hash();
+    int r = h->b.init(device, dims, nullptr, origin, voxel_size, trunc);
+    Table& t = h->t;
+    if (r == TSDF_OK) {
+        h->b.vol.shard = shard;
+        h->b.vol.n_shards = n_shards;
+        if (max_blocks <= 0) max_blocks = std::min<long long>(h->b.n_bricks, 1 << 16);
+        max_blocks = std::max<long long>(max_blocks, 64);
+        t.capacity = capacity;
+        t.max_blocks = max_blocks;
+        t.int_bits = int_bits;
+        t.overflow_cap = (int)std::min<long long>(h->b.n_bricks, 1ll << 30);
+        hipError_t e = hipMalloc(&t.keys, sizeof(unsigned long long) * capacity);
+        if (e == hipSuccess) e = hipMalloc(&t.vals, sizeof(int) * capacity);
+        if (e == hipSuccess) e = hipMalloc(&t.occ, sizeof(unsigned long long) * 8 * max_blocks);
+        if (e == hipSuccess) e = hipMalloc(&t.free_list, sizeof(int) * max_blocks);
+        if (e == hipSuccess) e = hipMalloc(&t.overflow, sizeof(int) * (size_t)t.overflow_cap);
+        if (e == hipSuccess) e = hipMalloc(&t.st, sizeof(PoolState));
+        if (e == hipSuccess) e = hipMalloc(&h->b.pool.tsdf, sizeof(float) * kBrickVox * max_blocks);
+        if (e == hipSuccess) e = hipMalloc(&h->b.pool.weight, sizeof(float) * kBrickVox * max_blocks);
+        if (e == hipSuccess) e = hipMalloc(&h->b.pool.color, sizeof(float) * kBrickVox * max_blocks);
+        if (e != hipSuccess)
+            r = set_error(e == hipErrorOutOfMemory ? TSDF_E_OOM : TSDF_E_HIP, "hash allocation: %s",
+                          hipGetErrorString(e));
+    }
+    if (r == TSDF_OK) r = tsdf_hash_reset(h);
+    if (r != TSDF_OK) {
+        std::string keep = tsdf_last_error();
+        tsdf_hash_destroy(h);
+        set_error(r, "%s", keep.c_str());
+        return r;
+    }
+    *out = h;
+    return TSDF_OK;
+}
+
+int tsdf_hash_destroy(tsdf_hash_t* h) {
+    if (!h) return TSDF_OK;
+    (void)hipSetDevice(h->b.device);
+    h->b.release();
+    void* ps[] = {h->t.keys, h->t.vals, h->t.occ, h->t.free_list, h->t.overflow, h->t.st,
+                  h->b.pool.tsdf, h->b.pool.weight, h->b.pool.color, h->d_list};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    delete h;
+    return TSDF_OK;
+}
+
+int tsdf_hash_reset(tsdf_hash_t* h) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, h->t.keys, (long long)h->t.capacity);
+    TSDF_HIP(hipGetLastError());
+    TSDF_HIP(hipMemsetAsync(h->t.st, 0, sizeof(PoolState), B.stream));
+    TSDF_HIP(hipMemsetAsync(B.stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    B.frames = 0;
+    std::memset(&h->host_st, 0, sizeof(h->host_st));
+    return TSDF_OK;
+}
+
+int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const void* color,
+                        int color_kind, int height, int width, const double K[9],
+                        const double world_to_cam[16], int flags) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    return hash_run(h, 1, depth, depth_kind, color, color_kind, height, width, K, world_to_cam, flags);
+}
+
+int tsdf_hash_integrate_batch(tsdf_hash_t* h, int n_frames, const void* depth, int depth_kind,
+                              const void* color, int color_kind, int height, int width,
+                              const double K[9], const double* world_to_cam, int flags) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    if (n_frames < 0) return set_error(TSDF_E_ARG, "n_frames < 0");
+    if (n_frames == 0) return TSDF_OK;
+    TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    return hash_run(h, n_frames, depth, depth_kind, color, color_kind, height, width, K,
+                    world_to_cam, flags);
+}
+
+int tsdf_hash_lookup(tsdf_hash_t* h, const int64_t* ijk, int64_t n, float* tsdf_, float* weight_,
+                     float* color_, uint8_t* found) {
+    if (!h || (n > 0 && (!ijk || !found)) || n < 0) return set_error(TSDF_E_ARG, "bad arguments");
+    if (n == 0) return TSDF_OK;
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    DevBufs bufs;
+    void *dijk, *dt = nullptr, *dw = nullptr, *dc = nullptr, *df = nullptr;
+    TSDF_TRY(upload(h, ijk, sizeof(int64_t) * 3 * n, &dijk));
+    bufs.add(dijk);
+    if (tsdf_) { TSDF_HIP(hipMalloc(&dt, sizeof(float) * n)); bufs.add(dt); }
+    if (weight_) { TSDF_HIP(hipMalloc(&dw, sizeof(float) * n)); bufs.add(dw); }
+    if (color_) { TSDF_HIP(hipMalloc(&dc, sizeof(float) * n)); bufs.add(dc); }
+    TSDF_HIP(hipMalloc(&df, n));
+    bufs.add(df);
+    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, B.stream, B.vol, h->t,
+                       B.pool, (const long long*)dijk, (long long)n, (float*)dt, (float*)dw, (float*)dc,
+                       (unsigned char*)df);
+    TSDF_HIP(hipGetLastError());
+    if (tsdf_) TSDF_HIP(hipMemcpyAsync(tsdf_, dt, sizeof(float) * n, hipMemcpyDeviceToHost, B.stream));
+    if (weight_) TSDF_HIP(hipMemcpyAsync(weight_, dw, sizeof(float) * n, hipMemcpyDeviceToHost, B.stream));
+    if (color_) TSDF_HIP(hipMemcpyAsync(color_, dc, sizeof(float) * n, hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipMemcpyAsync(found, df, n, hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    return TSDF_OK;
+}
+
+int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float* tsdf_,
+                     const float* weight_, const float* color_, int64_t* slot, int32_t* local) {
+    if (!h || n < 0 || (n > 0 && !ijk)) return set_error(TSDF_E_ARG, "bad arguments");
+    if (n == 0) return TSDF_OK;
+    Base& B = h->b;
+    const Vol& v = B.vol;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
+        if (x < 0 || y < 0 || z < 0 || x >= v.dims[0] || y >= v.dims[1] || z >= v.dims[2])
+            return set_error(TSDF_E_ARG, "voxel (%lld,%lld,%lld) outside the volume %dx%dx%d",
+                             (long long)x, (long long)y, (long long)z, v.dims[0], v.dims[1], v.dims[2]);
+    }
+    TSDF_HIP(hipSetDevice(B.device));
+    std::vector<unsigned long long> keys = unique_blocks(v, ijk, n);
+    const long long nk = (long long)keys.size();
+    // room first (the reference resizes before inserting, hash_fusion.py:208-209)
+    TSDF_TRY(read_state(h));
+    InfoDev inf{};
+    TSDF_TRY(info_raw(h, &inf));
+    while ((double)(inf.used + inf.tomb + nk) >= 0.75 * (double)h->t.capacity) {
+        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+        TSDF_TRY(info_raw(h, &inf));
+    }
+    if (h->host_st.pool_top + nk > h->t.max_blocks - h->host_st.free_count)
+        TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * nk)));
+    DevBufs bufs;
+    void *dkeys, *dblk = nullptr, *dslot = nullptr, *dijk, *dt, *dw, *dc;
+    TSDF_TRY(upload(h, keys.data(), sizeof(unsigned long long) * nk, &dkeys));
+    bufs.add(dkeys);
+    TSDF_HIP(hipMalloc(&dblk, sizeof(int) * nk));
+    bufs.add(dblk);
+    TSDF_HIP(hipMalloc(&dslot, sizeof(long long) * nk));
+    bufs.add(dslot);
+    hipLaunchKernelGGL(k_insert_blocks, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, B.stream, h->t,
+                       B.pool, (const unsigned long long*)dkeys, (long long)nk, (int*)dblk, (long long*)dslot);
+    TSDF_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+    TSDF_HIP(hipGetLastError());
+    TSDF_TRY(upload(h, ijk, sizeof(int64_t) * 3 * n, &dijk));
+    bufs.add(dijk);
+    TSDF_TRY(upload(h, tsdf_, tsdf_ ? sizeof(float) * n : 0, &dt));
+    bufs.add(dt);
+    TSDF_TRY(upload(h, weight_, weight_ ? sizeof(float) * n : 0, &dw));
+    bufs.add(dw);
+    TSDF_TRY(upload(h, color_, color_ ? sizeof(float) * n : 0, &dc));
+    bufs.add(dc);
+    hipLaunchKernelGGL(k_set_voxels, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, B.stream, B.vol, h->t,
+                       B.pool, (const long long*)dijk, (long long)n, (const float*)dt, (const float*)dw,
+                       (const float*)dc);
+    TSDF_HIP(hipGetLastError());
+    std::vector<int> blk(nk);
+    std::vector<long long> sl(nk);
+    TSDF_HIP(hipMemcpyAsync(blk.data(), dblk, sizeof(int) * nk, hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipMemcpyAsync(sl.data(), dslot, sizeof(long long) * nk, hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    for (long long i = 0; i < nk; ++i)
+        if (blk[i] < 0) return set_error(TSDF_E_CAPACITY, "hash insert failed (table or pool full)");
+    if (slot || local) {
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
+            const unsigned long long k = pack_key((int)(x >> 3), (int)(y >> 3), (int)(z >> 3));
+            const long long j = std::lower_bound(keys.begin(), keys.end(), k) - keys.begin();
+            if (slot) slot[i] = sl[j];
+            if (local) local[i] = (int32_t)((z & 7) * 64 + (x & 7) * 8 + (y & 7));
+        }
+    }
+    return TSDF_OK;
+}
+
+int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* removed) {
+    if (!h || n < 0 || (n > 0 && !ijk)) return set_error(TSDF_E_ARG, "bad arguments");
+    if (n == 0) return TSDF_OK;
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    std::vector<unsigned long long> keys = unique_blocks(B.vol, ijk, n);
+    DevBufs bufs;
+    void *dijk, *dkeys, *drem = nullptr;
+    TSDF_TRY(upload(h, ijk, sizeof(int64_t) * 3 * n, &dijk));
+    bufs.add(dijk);
+    if (removed) {
+        TSDF_HIP(hipMalloc(&drem, n));
+        bufs.add(drem);
+    }
+    hipLaunchKernelGGL(k_remove_voxels, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, B.stream, B.vol,
+                       h->t, (const long long*)dijk, (long long)n, (unsigned char*)drem);
+    TSDF_HIP(hipGetLastError());
+    if (!keys.empty()) {
+        TSDF_TRY(upload(h, keys.data(), sizeof(unsigned long long) * keys.size(), &dkeys));
+        bufs.add(dkeys);
+        hipLaunchKernelGGL(k_free_empty, dim3((unsigned)((keys.size() + 255) / 256)), dim3(256), 0, B.stream,
+                           h->t, (const unsigned long long*)dkeys, (long long)keys.size());
+        TSDF_HIP(hipGetLastError());
+    }
+    if (removed) TSDF_HIP(hipMemcpyAsync(removed, drem, n, hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    return TSDF_OK;
+}
+
+int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    InfoDev inf{};
+    TSDF_TRY(info_raw(h, &inf));
+    if (new_capacity <= (int64_t)inf.used) return set_error(TSDF_E_ARG, "new capacity too small");
+    return resize_table(h, new_capacity);
+}
+
+int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out) {
+    if (!h || !out) return set_error(TSDF_E_ARG, "null pointer");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    InfoDev inf{};
+    TSDF_TRY(info_raw(h, &inf));
+    TSDF_TRY(read_state(h));
+    out->capacity = h->t.capacity;
+    out->used = (int64_t)inf.used;
+    out->tombstones = (int64_t)inf.tomb;
+    out->displaced = (int64_t)inf.displaced;
+    out->max_probe = (int64_t)inf.max_probe;
+    out->blocks_in_pool = h->host_st.pool_top;
+    out->pool_capacity = h->t.max_blocks;
+    out->entries = (int64_t)inf.entries;
+    return TSDF_OK;
+}
+
+int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf_, float* weight_, float* color_) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    const size_t n = (size_t)B.vol.dims[0] * B.vol.dims[1] * B.vol.dims[2];
+    DevBufs bufs;
+    void *dt = nullptr, *dw = nullptr, *dc = nullptr;
+    if (tsdf_) { TSDF_HIP(hipMalloc(&dt, n * sizeof(float))); bufs.add(dt); }
+    if (weight_) { TSDF_HIP(hipMalloc(&dw, n * sizeof(float))); bufs.add(dw); }
+    if (color_) { TSDF_HIP(hipMalloc(&dc, n * sizeof(float))); bufs.add(dc); }
+    hipLaunchKernelGGL(k_fill_dense, dim3(4096), dim3(256), 0, B.stream, (float*)dt, (float*)dw, (float*)dc, n);
+    TSDF_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_to_dense, dim3(4096), dim3(256), 0, B.stream, B.vol, h->t, B.pool, (float*)dt,
+                       (float*)dw, (float*)dc);
+    TSDF_HIP(hipGetLastError());
+    if (tsdf_) TSDF_HIP(hipMemcpyAsync(tsdf_, dt, n * sizeof(float), hipMemcpyDeviceToHost, B.stream));
+    if (weight_) TSDF_HIP(hipMemcpyAsync(weight_, dw, n * sizeof(float), hipMemcpyDeviceToHost, B.stream));
+    if (color_) TSDF_HIP(hipMemcpyAsync(color_, dc, n * sizeof(float), hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    return TSDF_OK;
+}
+
+int tsdf_hash_sync(tsdf_hash_t* h) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_HIP(hipStreamSynchronize(h->b.stream));
+    return TSDF_OK;
+}
+
+int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    return h->b.read_stats(out, reset);
+}
+
+int tsdf_hash_set_profiling(tsdf_hash_t* h, int on) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    return h->b.set_profiling(on);
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// tsdf_host.h -- host-side internals shared by the dense and hash C-ABI implementations.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "tsdf_device.h"
+#include "tsdf_hip.h"
+
+namespace tsdf {
+
+int set_error(int code, const char* fmt, ...);
+
+#define TSDF_HIP(expr)                                                                        \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return ::tsdf::set_error(e_ == hipErrorOutOfMemory ? TSDF_E_OOM : TSDF_E_HIP,     \
+                                     "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                                     __FILE__, __LINE__);                                     \
+    } while (0)
+
+#define TSDF_TRY(expr)            \
+    do {                          \
+        int r_ = (expr);          \
+        if (r_ != TSDF_OK) return r_; \
+    } while (0)
+
+struct PyrLayout {
+    int off[kPyrLevels + 1];
+    int w[kPyrLevels + 1];
+    int h[kPyrLevels + 1];
+    int total;
+};
+PyrLayout pyr_layout(int H, int W);
+
+// HIP-event timing of the integrate kernels (tsdf_*_set_profiling).
+struct Profiler {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<hipEvent_t> spare;
+    double ms = 0.0;
+    long long launches = 0;
+    int begin(hipStream_t s, hipEvent_t* e0);
+    int end(hipStream_t s, hipEvent_t e0);
+    int collect();  // synchronises on the recorded events and accumulates their spans
+    void release();
+};
+
+// State common to the dense and hash handles.
+struct Base {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Vol vol{};
+    Pool pool{};
+    long long n_bricks = 0;
+    float* pyr = nullptr;
+    int pyr_H = 0, pyr_W = 0;
+    PyrLayout lay{};
+    unsigned long long* stats = nullptr;  // kNStat x kStatSpread
+    long long frames = 0;
+    Profiler prof;
+    // staging for host-pointer frames
+    void* st_depth = nullptr;
+    size_t st_depth_bytes = 0;
+    void* st_color = nullptr;
+    size_t st_color_bytes = 0;
+
+    int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
+             double vs, double trunc);
+    int ensure_pyr(int H, int W);
+    // Builds the frame constants, staging host inputs to the device when needed.
+    int prepare_frame(Frame* fr, const void* depth, int dk, const void* color, int ck, int H,
+                      int W, const double K[9], const double Tinv[16], double ow, int flags,
+                      int frame_index);
+    int launch_pyramid(const Frame& fr, int dk);
+    int read_stats(tsdf_stats_t* out, int reset);
+    int set_profiling(int on);
+    void release();
+};
+
+int check_frame_args(const void* depth, int dk, const void* color, int ck, int H, int W,
+                     const double* K, const double* Tinv);
+
+}  // namespace tsdf

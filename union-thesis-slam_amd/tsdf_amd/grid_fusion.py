@@ -1,0 +1,200 @@
+"""Dense TSDF volume on MI355X -- drop-in for `grid_fusion.TSDFVolume` (grid_fusion.py:19-320).
+
+Same constructor, same `integrate()` / `get_volume()` signatures and results as the
+reference's CPU path (bit-exact voxel set, tsdf, weight and colour; tests/test_dense_gpu.py).
+The work runs in hand-written gfx950 kernels behind the C-ABI of include/tsdf_hip.h; this
+module only does the reference's host-side duties:
+
+  * volume geometry, including the in-place rewrite of vol_bnds[:,1] (grid_fusion.py:31-44);
+  * inv(cam_pose) with NumPy/LAPACK, as the reference does on the host (grid_fusion.py:265);
+  * the colour fold for non-uint8 input (grid_fusion.py:228-232);
+  * depth: uint16 millimetres are sent when they reproduce the float64 metres exactly
+    (mm / 1000.0 == depth bit for bit, the demos' ingest), else the float64 metres themselves.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _ffi
+
+
+def volume_geometry(vol_bnds, voxel_size):
+    """grid_fusion.py:31-44: dims = ceil(extent/vs), vol_bnds[:,1] rewritten in place,
+    origin = f32(vol_bnds[:,0])."""
+    vol_bnds = np.asarray(vol_bnds)
+    assert vol_bnds.shape == (3, 2), "[!] `vol_bnds` should be of shape (3, 2)."
+    vs = float(voxel_size)
+    dims = np.ceil((vol_bnds[:, 1] - vol_bnds[:, 0]) / vs).copy(order="C").astype(int)
+    vol_bnds[:, 1] = vol_bnds[:, 0] + dims * vs
+    origin = vol_bnds[:, 0].copy(order="C").astype(np.float32)
+    return vol_bnds, dims, origin, vs
+
+
+def encode_depth(depth_im):
+    """(kind, contiguous array) for the C-ABI.  uint16 input is taken as millimetres."""
+    d = np.asarray(depth_im)
+    if d.dtype == np.uint16:
+        return _ffi.DEPTH_U16_MM, np.ascontiguousarray(d)
+    d = np.ascontiguousarray(d, dtype=np.float64)
+    with np.errstate(invalid="ignore", over="ignore"):
+        mm = np.rint(d * 1000.0)
+        ok = bool(np.all((mm >= 0) & (mm <= 65535)))
+        if ok:
+            mm16 = mm.astype(np.uint16)
+            if np.array_equal((mm16.astype(np.float64) / 1000.0).view(np.uint64), d.view(np.uint64)):
+                return _ffi.DEPTH_U16_MM, mm16
+    return _ffi.DEPTH_F64_M, d
+
+
+def encode_color(color_im):
+    """uint8 RGB goes as is (the kernel folds it); anything else is folded here exactly like
+    grid_fusion.py:228-232 and sent as float32."""
+    c = np.asarray(color_im)
+    if c.dtype == np.uint8 and c.ndim == 3 and c.shape[2] == 3:
+        return _ffi.COLOR_RGB8, np.ascontiguousarray(c)
+    c = c.astype(np.float32)
+    folded = np.floor(c[..., 2] * (256 * 256) + c[..., 1] * 256 + c[..., 0])
+    return _ffi.COLOR_F32, np.ascontiguousarray(folded, dtype=np.float32)
+
+
+class TSDFVolume:
+    """Volumetric TSDF Fusion of RGB-D Images, on an MI355X.
+
+    Args (as grid_fusion.py:22-29):
+      vol_bnds (ndarray): (3, 2) xyz bounds (min/max) in metres; column 1 is rewritten.
+      voxel_size (float): metres.
+      use_gpu: accepted for signature compatibility; the volume always lives in HBM.
+    Extra keyword-only args (slab sharding):
+      device: HIP device index.  slab: (x_begin, x_end) voxel range of this shard along x.
+    """
+
+    def __init__(self, vol_bnds, voxel_size, use_gpu=True, *, device=0, slab=None):
+        print("Initializing voxel grids ... ")
+        self._vol_bnds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
+            vol_bnds, voxel_size)
+        self._trunc_margin = 5 * self._voxel_size
+        self._color_const = 256 * 256
+        print("Voxel volume size: {} x {} x {} - # points: {:,}".format(
+            self._vol_dim[0], self._vol_dim[1], self._vol_dim[2],
+            self._vol_dim[0] * self._vol_dim[1] * self._vol_dim[2]))
+        self.gpu_mode = True
+        self.device = int(device)
+        x0, x1 = (0, int(self._vol_dim[0])) if slab is None else (int(slab[0]), int(slab[1]))
+        if not (0 <= x0 < x1 <= int(self._vol_dim[0])):
+            raise ValueError(f"slab {slab} outside [0, {self._vol_dim[0]})")
+        self.slab = (x0, x1)
+        self._local_dim = np.array([x1 - x0, self._vol_dim[1], self._vol_dim[2]], np.int64)
+        dims = np.ascontiguousarray(self._local_dim, dtype=np.int64)
+        off = np.array([x0, 0, 0], np.int64)
+        h = ctypes.c_void_p()
+        _ffi.call("tsdf_dense_create", _ffi.ptr(dims), _ffi.ptr(off),
+                  _ffi.ptr(np.ascontiguousarray(self._vol_origin, dtype=np.float32)),
+                  self._voxel_size, float(self._trunc_margin), self.device, ctypes.byref(h))
+        self._h = h
+
+    # ------------------------------------------------------------------ reference API
+    def integrate(self, color_im, depth_im, cam_intr, cam_pose, obs_weight=1.):
+        """Integrate an RGB-D frame (grid_fusion.py:214-314).
+
+        color_im (H,W,3) RGB, depth_im (H,W) metres, cam_intr (3,3), cam_pose (4,4)
+        camera-to-world, obs_weight float."""
+        im_h, im_w = np.shape(depth_im)[:2]
+        dk, d = encode_depth(depth_im)
+        ck, c = encode_color(color_im)
+        if c.shape[:2] != (im_h, im_w):
+            raise ValueError("color_im and depth_im sizes differ")
+        K = _ffi.f64(cam_intr, 9)
+        Tinv = _ffi.f64(np.linalg.inv(np.asarray(cam_pose, dtype=np.float64)), 16)
+        _ffi.call("tsdf_dense_integrate", self._h, _ffi.ptr(d), dk, _ffi.ptr(c), ck, im_h, im_w,
+                  _ffi.ptr(K), _ffi.ptr(Tinv), float(obs_weight), 0)
+
+    def get_volume(self):
+        """(tsdf, colour) float32 C-order (X,Y,Z) host arrays (grid_fusion.py:316-320)."""
+        t, _, c = self.get_state(weight=False)
+        return t, c
+
+    # ------------------------------------------------------------------ extensions
+    def get_state(self, weight=True):
+        shape = tuple(int(x) for x in self._local_dim)
+        t = np.empty(shape, np.float32)
+        w = np.empty(shape, np.float32) if weight else None
+        c = np.empty(shape, np.float32)
+        _ffi.call("tsdf_dense_get", self._h, _ffi.ptr(t), _ffi.ptr(w), _ffi.ptr(c))
+        return t, w, c
+
+    def get_weight(self):
+        return self.get_state(weight=True)[1]
+
+    def set_state(self, tsdf, weight, color):
+        a = [None if x is None else np.ascontiguousarray(x, dtype=np.float32) for x in (tsdf, weight, color)]
+        _ffi.call("tsdf_dense_set", self._h, *[_ffi.ptr(x) for x in a])
+
+    def integrate_batch(self, depth, color, cam_intr, world_to_cam, obs_weight=None, *,
+                        depth_kind=_ffi.DEPTH_U16_MM, color_kind=_ffi.COLOR_RGB8, hw=None,
+                        device_ptrs=False, sync=True):
+        """F frames back to back on the volume's stream (the bench's step).
+
+        depth/color: host ndarrays (F,H,W[,3]) or, with device_ptrs=True, integer device
+        addresses of such arrays already resident in HBM (then hw=(H,W) is required).
+        world_to_cam: (F,4,4) = inv(cam_pose) per frame, computed by the caller."""
+        T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
+        n = T.shape[0]
+        H, W = hw if device_ptrs else np.shape(depth)[1:3]
+        ow = None if obs_weight is None else _ffi.f64(obs_weight, n)
+        flags = (_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC)
+        _ffi.call("tsdf_dense_integrate_batch", self._h, n, _ffi.ptr(depth), depth_kind,
+                  _ffi.ptr(color), color_kind, int(H), int(W), _ffi.ptr(_ffi.f64(cam_intr, 9)),
+                  _ffi.ptr(T), _ffi.ptr(ow), flags)
+
+    def sync(self):
+        _ffi.call("tsdf_dense_sync", self._h)
+
+    def stats(self, reset=False):
+        s = _ffi.Stats()
+        _ffi.call("tsdf_dense_stats", self._h, ctypes.byref(s), int(bool(reset)))
+        return s.as_dict()
+
+    def set_profiling(self, on=True):
+        _ffi.call("tsdf_dense_set_profiling", self._h, int(bool(on)))
+
+    def reset(self):
+        _ffi.call("tsdf_dense_reset", self._h)
+
+    def get_point_cloud(self):
+        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+
+    def get_mesh(self):
+        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _ffi.call("tsdf_dense_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rigid_transform(xyz, transform):
+    """grid_fusion.py:363-368 (host helper used by the demos' bounds estimation)."""
+    xyz_h = np.hstack([xyz, np.ones((len(xyz), 1), dtype=np.float32)])
+    xyz_t_h = np.dot(transform, xyz_h.T).T
+    return xyz_t_h[:, :3]
+
+
+def get_view_frustum(depth_im, cam_intr, cam_pose):
+    """grid_fusion.py:371-383: the camera origin and the four image corners pushed out to the
+    frame's max depth, in world coordinates, as a (3, 5) array."""
+    h, w = depth_im.shape[:2]
+    dmax = np.max(depth_im)
+    z = np.array([0.0, dmax, dmax, dmax, dmax])
+    u = np.array([0, 0, 0, w, w])
+    v = np.array([0, 0, h, 0, h])
+    cam = np.stack([(u - cam_intr[0, 2]) * z / cam_intr[0, 0],
+                    (v - cam_intr[1, 2]) * z / cam_intr[1, 1], z], axis=1)
+    return rigid_transform(cam, cam_pose).T

@@ -1,0 +1,256 @@
+"""Voxel-hash map on MI355X -- drop-in for `hash_fusion.HashTable` (hash_fusion.py:29-507).
+
+The reference hashes single voxels into 5-slot chained buckets and integrates with a Python
+loop (hash_fusion.py:134-145, ~45 us per voxel).  Here the map stores 8^3 voxel BLOCKS in an
+open-addressed table in HBM: the home slot of a block is the reference's hash_function of the
+block coordinates, a wave probes 64 slots per step and inserts with one CAS, and each block's
+512 voxels are integrated by one wave (csrc/tsdf_device.h).  What stays the same:
+
+  * hash_function(xyz) returns the reference's value for the same coordinates and table size
+    (int64 NumPy arithmetic, or int_bits=32 for the wrapping int32 of the author's run);
+  * integrate() updates exactly the voxels the reference updates (the same projection of every
+    voxel of the bounded volume), with obs_weight ignored as in hash_fusion.py:141,145, and the
+    same weight and colour; tsdf is stored as float32 (the reference keeps a float64 per voxel,
+    so tsdf agrees to ~1e-7, inside the 1e-4 parity bound);
+  * an "entry" is a voxel that was integrated or added; count_num_hash_entries, get_hash_entry,
+    add_hash_entry, remove and double_table_size keep their meaning.
+
+Known, documented differences: add_hash_entry of an existing position finds it
+instead of storing a duplicate (hash_map_test.py:68-75 stores 4000 copies of one key); load
+factor and collisions are counted over block slots, not 5-voxel buckets.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _ffi
+from .data_structures import HashEntry, Voxel
+from .grid_fusion import encode_color, encode_depth, volume_geometry
+
+P1 = 73856093
+P2 = 19349669
+P3 = 83492791
+
+
+class HashTable:
+    """The data structure for voxel storage and retrieval: a GPU hash table of voxel blocks.
+
+    Args as hash_fusion.py:34: vol_bounds (3,2) metres (column 1 rewritten in place),
+    voxel_size, map_size (table slots), load_factor / use_gpu (accepted, ignored like the
+    reference).  Keyword-only: int_bits (64|32), max_blocks (initial pool size; grows),
+    device, shard / n_shards (bucket-range ownership for multi-GPU).
+    """
+
+    def __init__(self, vol_bounds, voxel_size, map_size=1000000, load_factor=0.75, use_gpu=False,
+                 *, int_bits=64, max_blocks=None, device=0, shard=0, n_shards=1):
+        self._load_factor = 0.75
+        self._vol_bounds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
+            vol_bounds, voxel_size)
+        self._trunc_margin = 5 * self._voxel_size
+        self._color_const = 256 * 256
+        print("Voxel volume size: {} x {} x {} - # points: {:,}".format(
+            self._vol_dim[0], self._vol_dim[1], self._vol_dim[2],
+            self._vol_dim[0] * self._vol_dim[1] * self._vol_dim[2]))
+        self.int_bits = int(int_bits)
+        self.device = int(device)
+        nb = int(np.prod((np.asarray(self._vol_dim) + 7) // 8))
+        if max_blocks is None:
+            max_blocks = min(nb, 1 << 16)
+        h = ctypes.c_void_p()
+        _ffi.call("tsdf_hash_create", _ffi.ptr(np.ascontiguousarray(self._vol_dim, dtype=np.int64)),
+                  _ffi.ptr(np.ascontiguousarray(self._vol_origin, dtype=np.float32)),
+                  float(self._voxel_size), float(self._trunc_margin), int(map_size),
+                  int(max_blocks), self.int_bits, int(shard), int(n_shards), self.device,
+                  ctypes.byref(h))
+        self._h = h
+
+    # ------------------------------------------------------------------ table geometry
+    @property
+    def _table_size(self) -> int:
+        return self.info()["capacity"]
+
+    def info(self) -> dict:
+        s = _ffi.HashInfo()
+        _ffi.call("tsdf_hash_info", self._h, ctypes.byref(s))
+        return s.as_dict()
+
+    # ------------------------------------------------------------------ integrate
+    def integrate(self, color_im, depth_im, cam_intr, cam_pose, obs_weight=1.):
+        """hash_fusion.py:103-145 -- obs_weight is ignored exactly like the reference."""
+        im_h, im_w = np.shape(depth_im)[:2]
+        dk, d = encode_depth(depth_im)
+        ck, c = encode_color(color_im)
+        K = _ffi.f64(cam_intr, 9)
+        Tinv = _ffi.f64(np.linalg.inv(np.asarray(cam_pose, dtype=np.float64)), 16)
+        _ffi.call("tsdf_hash_integrate", self._h, _ffi.ptr(d), dk, _ffi.ptr(c), ck, im_h, im_w,
+                  _ffi.ptr(K), _ffi.ptr(Tinv), 0)
+
+    def integrate_batch(self, depth, color, cam_intr, world_to_cam, *, depth_kind=_ffi.DEPTH_U16_MM,
+                        color_kind=_ffi.COLOR_RGB8, hw=None, device_ptrs=False, sync=True):
+        T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
+        H, W = hw if device_ptrs else np.shape(depth)[1:3]
+        flags = (_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC)
+        _ffi.call("tsdf_hash_integrate_batch", self._h, T.shape[0], _ffi.ptr(depth), depth_kind,
+                  _ffi.ptr(color), color_kind, int(H), int(W), _ffi.ptr(_ffi.f64(cam_intr, 9)),
+                  _ffi.ptr(T), flags)
+
+    # ------------------------------------------------------------------ statistics
+    def count_num_hash_entries(self) -> int:
+        return int(self.info()["entries"])
+
+    def get_num_non_empty_bucket(self) -> int:
+        return int(self.info()["used"])
+
+    get_num_non_empty_buckets = get_num_non_empty_bucket
+
+    def needs_resize(self) -> bool:
+        i = self.info()
+        return i["used"] / i["capacity"] >= self._load_factor
+
+    def get_load_factor(self) -> float:
+        i = self.info()
+        return i["used"] / i["capacity"]
+
+    def get_num_collisions(self) -> int:
+        """Block keys displaced from their home slot (the open-addressing analogue of the
+        reference's 'buckets holding more than one entry', hash_fusion.py:169-180)."""
+        return int(self.info()["displaced"])
+
+    # ------------------------------------------------------------------ keys
+    def hash_function(self, world_coord):
+        """hash_fusion.py:182-190 for one coordinate triple (computed on the device)."""
+        return int(self.hash_keys(np.asarray(world_coord, dtype=np.int64).reshape(1, 3))[0])
+
+    def hash_keys(self, coords, table_size=None):
+        xyz = np.ascontiguousarray(np.asarray(coords, dtype=np.int64).reshape(-1, 3))
+        out = np.empty(xyz.shape[0], np.int64)
+        n = self._table_size if table_size is None else int(table_size)
+        _ffi.call("tsdf_hash_keys", _ffi.ptr(xyz), xyz.shape[0], n, self.int_bits, _ffi.ptr(out),
+                  self.device)
+        return out
+
+    # ------------------------------------------------------------------ entries
+    @staticmethod
+    def _ijk(positions):
+        return np.ascontiguousarray(np.asarray(positions, dtype=np.int64).reshape(-1, 3))
+
+    def add_voxel(self, voxel, world_coord):
+        self.add_hash_entry(HashEntry(world_coord, None, voxel))
+
+    def add_hash_entry(self, hash_entry):
+        """Insert the entry's voxel; returns (table slot, voxel-in-block) -- the reference's
+        (bucket, slot) -- or (-1, -1) for None."""
+        if hash_entry is None:
+            return -1, -1
+        ijk = self._ijk(hash_entry.get_position())
+        v = hash_entry.get_voxel()
+        vals = [None, None, None]
+        if v is not None and v.get_sdf() is not None:
+            vals = [np.array([float(v.get_sdf())], np.float32), np.array([float(v.get_weight())], np.float32),
+                    np.array([float(v.get_color())], np.float32)]
+        slot = np.empty(1, np.int64)
+        local = np.empty(1, np.int32)
+        _ffi.call("tsdf_hash_insert", self._h, _ffi.ptr(ijk), 1, *[_ffi.ptr(a) for a in vals],
+                  _ffi.ptr(slot), _ffi.ptr(local))
+        hash_entry.set_offset((int(slot[0]), int(local[0])))
+        return int(slot[0]), int(local[0])
+
+    def add_entries(self, positions, tsdf=None, weight=None, color=None):
+        """Batched add_hash_entry: (n,3) voxel indices, optional per-voxel values."""
+        ijk = self._ijk(positions)
+        n = ijk.shape[0]
+        arr = [None if a is None else np.ascontiguousarray(np.asarray(a, np.float32).reshape(n))
+               for a in (tsdf, weight, color)]
+        slot = np.empty(n, np.int64)
+        local = np.empty(n, np.int32)
+        _ffi.call("tsdf_hash_insert", self._h, _ffi.ptr(ijk), n, *[_ffi.ptr(a) for a in arr],
+                  _ffi.ptr(slot), _ffi.ptr(local))
+        return slot, local
+
+    def lookup(self, positions):
+        """Batched get_hash_entry: (found bool, tsdf, weight, colour) arrays."""
+        ijk = self._ijk(positions)
+        n = ijk.shape[0]
+        t, w, c = (np.empty(n, np.float32) for _ in range(3))
+        f = np.empty(n, np.uint8)
+        _ffi.call("tsdf_hash_lookup", self._h, _ffi.ptr(ijk), n, _ffi.ptr(t), _ffi.ptr(w),
+                  _ffi.ptr(c), _ffi.ptr(f))
+        return f.astype(bool), t, w, c
+
+    def get_hash_entry(self, world_coord):
+        found, t, w, c = self.lookup(world_coord)
+        if not found[0]:
+            return None
+        return HashEntry(list(np.asarray(world_coord).reshape(3)), None,
+                         Voxel(float(t[0]), float(c[0]), float(w[0])))
+
+    def get_voxel(self, world_coord):
+        e = self.get_hash_entry(world_coord)
+        return None if e is None else e.get_voxel()
+
+    def remove_entries(self, positions):
+        ijk = self._ijk(positions)
+        r = np.empty(ijk.shape[0], np.uint8)
+        _ffi.call("tsdf_hash_remove", self._h, _ffi.ptr(ijk), ijk.shape[0], _ffi.ptr(r))
+        return r.astype(bool)
+
+    def remove(self, world_coord):
+        self.remove_hash_entry(HashEntry(world_coord, None, None))
+
+    def remove_hash_entry(self, hash_entry):
+        """1 if removed, 0 if absent (hash_fusion.py:330-385)."""
+        return int(self.remove_entries(hash_entry.get_position())[0])
+
+    def double_table_size(self):
+        n = self._table_size
+        print("Resizing hash table from {} to {}".format(n, n * 2))
+        _ffi.call("tsdf_hash_resize", self._h, 2 * n)
+        print("Resize finished.")
+
+    # ------------------------------------------------------------------ export
+    def get_volume(self):
+        """hash_fusion.py:442-463: dense (tsdf, colour) float32 arrays of vol_dim."""
+        t, _, c = self.get_state(weight=False)
+        return t, c
+
+    def get_state(self, weight=True):
+        shape = tuple(int(x) for x in self._vol_dim)
+        t = np.empty(shape, np.float32)
+        w = np.empty(shape, np.float32) if weight else None
+        c = np.empty(shape, np.float32)
+        _ffi.call("tsdf_hash_get_dense", self._h, _ffi.ptr(t), _ffi.ptr(w), _ffi.ptr(c))
+        return t, w, c
+
+    def get_mesh(self):
+        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+
+    def get_point_cloud(self):
+        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+
+    # ------------------------------------------------------------------ misc
+    def sync(self):
+        _ffi.call("tsdf_hash_sync", self._h)
+
+    def stats(self, reset=False):
+        s = _ffi.Stats()
+        _ffi.call("tsdf_hash_stats", self._h, ctypes.byref(s), int(bool(reset)))
+        return s.as_dict()
+
+    def set_profiling(self, on=True):
+        _ffi.call("tsdf_hash_set_profiling", self._h, int(bool(on)))
+
+    def reset(self):
+        _ffi.call("tsdf_hash_reset", self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _ffi.call("tsdf_hash_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
