@@ -60,6 +60,8 @@ typedef struct {
     int64_t lookups;          /* hash: block lookups performed */
     double kernel_ms;         /* integrate-kernel time from HIP events (profiling on only) */
     int64_t kernel_launches;  /* integrate-kernel launches timed */
+    int64_t bricks_skipped;   /* hash: bricks skipped for lack of table/pool space (must be 0
+                                 after a synchronous call; see tsdf_hash_integrate_batch) */
 } tsdf_stats_t;
 
 typedef struct {

@@ -115,6 +115,10 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];
     if (n_bricks >= (1ll << 31)) return set_error(TSDF_E_ARG, "too many bricks");
     TSDF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    TSDF_HIP(hipMalloc(&list, sizeof(int) * (size_t)n_bricks));
+    TSDF_HIP(hipMalloc(&count, sizeof(unsigned int) * 4));
+    TSDF_HIP(hipMemsetAsync(count, 0, sizeof(unsigned int) * 4, stream));
     TSDF_HIP(hipMalloc(&stats, sizeof(unsigned long long) * kNStat * kStatSpread));
     TSDF_HIP(hipMemsetAsync(stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, stream));
     return TSDF_OK;
@@ -125,10 +129,16 @@ int Base::ensure_pyr(int H, int W) {
     if (pyr) {
         TSDF_HIP(hipStreamSynchronize(stream));
         TSDF_HIP(hipFree(pyr));
+        TSDF_HIP(hipFree(depthm));
+        TSDF_HIP(hipFree(rgbx));
         pyr = nullptr;
+        depthm = nullptr;
+        rgbx = nullptr;
     }
     lay = pyr_layout(H, W);
     TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total));
+    TSDF_HIP(hipMalloc(&depthm, sizeof(double) * (size_t)H * W));
+    TSDF_HIP(hipMalloc(&rgbx, sizeof(unsigned) * (size_t)H * W));
     pyr_H = H;
     pyr_W = W;
     return TSDF_OK;
@@ -181,7 +191,9 @@ int Base::prepare_frame(Frame* fr, const void* depth, int dk, const void* color,
     fr->H = H;
     fr->W = W;
     fr->depth = d;
+    fr->depthm = dk == TSDF_DEPTH_U16_MM ? depthm : (const double*)d;
     fr->color = c;
+    fr->rgbx = rgbx;
     fr->pyr = pyr;
     for (int L = 0; L <= kPyrLevels; ++L) {
         fr->pyr_off[L] = lay.off[L];
@@ -191,14 +203,28 @@ int Base::prepare_frame(Frame* fr, const void* depth, int dk, const void* color,
     return TSDF_OK;
 }
 
-int Base::launch_pyramid(const Frame& fr, int dk) {
+int Base::launch_prep(const Frame& fr, int dk, int ck) {
     dim3 grid((fr.W + 63) / 64, (fr.H + 63) / 64);
-    if (dk == TSDF_DEPTH_U16_MM)
-        hipLaunchKernelGGL(k_pyramid<0>, grid, dim3(kWG), 0, stream, fr, pyr);
+    if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
+        hipLaunchKernelGGL((k_prep<0, 0>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
+    else if (dk == TSDF_DEPTH_U16_MM)
+        hipLaunchKernelGGL((k_prep<0, 1>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
+    else if (ck == TSDF_COLOR_RGB8)
+        hipLaunchKernelGGL((k_prep<1, 0>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
     else
-        hipLaunchKernelGGL(k_pyramid<1>, grid, dim3(kWG), 0, stream, fr, pyr);
+        hipLaunchKernelGGL((k_prep<1, 1>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
     TSDF_HIP(hipGetLastError());
     return TSDF_OK;
+}
+
+unsigned Base::grid_for(const void* kernel) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWG, 0) != hipSuccess || per_cu < 1)
+        per_cu = 4;
+    long long g = (long long)per_cu * n_cu;
+    const long long need = (n_bricks + (kWG / 64) - 1) / (kWG / 64);
+    if (g > need) g = need;
+    return (unsigned)(g < 1 ? 1 : g);
 }
 
 int Base::read_stats(tsdf_stats_t* out, int reset) {
@@ -226,6 +252,7 @@ int Base::read_stats(tsdf_stats_t* out, int reset) {
     out->lookups = (int64_t)s[ST_LOOKUPS];
     out->kernel_ms = prof.ms;
     out->kernel_launches = prof.launches;
+    out->bricks_skipped = (int64_t)s[ST_OVERFLOW];
     if (reset) {
         TSDF_HIP(hipMemsetAsync(stats, 0, sizeof(unsigned long long) * h.size(), stream));
         TSDF_HIP(hipStreamSynchronize(stream));
@@ -246,11 +273,19 @@ void Base::release() {
     if (stream) (void)hipStreamSynchronize(stream);
     prof.release();
     if (pyr) (void)hipFree(pyr);
+    if (depthm) (void)hipFree(depthm);
+    if (rgbx) (void)hipFree(rgbx);
+    if (list) (void)hipFree(list);
+    if (count) (void)hipFree(count);
     if (stats) (void)hipFree(stats);
     if (st_depth) (void)hipFree(st_depth);
     if (st_color) (void)hipFree(st_color);
     if (stream) (void)hipStreamDestroy(stream);
     pyr = nullptr;
+    depthm = nullptr;
+    rgbx = nullptr;
+    list = nullptr;
+    count = nullptr;
     stats = nullptr;
     st_depth = st_color = nullptr;
     stream = nullptr;

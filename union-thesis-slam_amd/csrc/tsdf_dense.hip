@@ -1,6 +1,6 @@
 // tsdf_dense.hip -- dense TSDF grid: the MI355X replacement of TSDFVolume
 // (grid_fusion.py:19-320).  HBM layout: three f32 SoA arrays of 512-voxel bricks, brick b =
-// (bx*nby + by)*nbz + bz, brick-local voxel z*64 + x*8 + y.
+// (bx*nby + by)*nbz + bz, brick-local voxel (x*8 + y)*8 + z.
 #include <cstring>
 
 #include "tsdf_host.h"
@@ -33,7 +33,7 @@ __global__ void k_relayout(Vol v, const float* __restrict__ src, float* __restri
         const int y = (int)(xy % v.dims[1]);
         const int x = (int)(xy / v.dims[1]);
         const size_t b = ((size_t)(x >> 3) * v.nb[1] + (y >> 3)) * v.nb[2] + (z >> 3);
-        const size_t j = b * kBrickVox + (size_t)(z & 7) * 64 + (x & 7) * 8 + (y & 7);
+        const size_t j = b * kBrickVox + (size_t)((x & 7) * 8 + (y & 7)) * 8 + (z & 7);
         if (TO_CORDER) dst[i] = src[j];
         else dst[j] = src[i];
     }
@@ -44,22 +44,25 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
     const Table no_table{};
-    const unsigned grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    const unsigned grid0 = B.grid_for((const void*)k_integrate<false, 0>);
+    const unsigned grid1 = B.grid_for((const void*)k_integrate<false, 1>);
     for (int f = 0; f < n_frames; ++f) {
         Frame fr;
         TSDF_TRY(B.prepare_frame(&fr, depth, dk, color, ck, H, W, K, Tinv + 16 * (size_t)f,
                                  ow ? ow[f] : 1.0, flags, f));
-        TSDF_TRY(B.launch_pyramid(fr, dk));
+        TSDF_TRY(B.launch_prep(fr, dk, ck));
+        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, fr, no_table,
+                           B.list, B.count, B.stats);
+        TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
-        if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
-            hipLaunchKernelGGL((k_integrate<false, 0, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
-        else if (dk == TSDF_DEPTH_U16_MM)
-            hipLaunchKernelGGL((k_integrate<false, 0, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
-        else if (ck == TSDF_COLOR_RGB8)
-            hipLaunchKernelGGL((k_integrate<false, 1, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
+        if (ck == TSDF_COLOR_RGB8)
+            hipLaunchKernelGGL((k_integrate<false, 0>), dim3(grid0), dim3(kWG), 0, B.stream, B.vol, fr, B.pool,
+                               no_table, B.stats, (const int*)B.list, B.count, 0);
         else
-            hipLaunchKernelGGL((k_integrate<false, 1, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, no_table, B.stats, nullptr, 0);
+            hipLaunchKernelGGL((k_integrate<false, 1>), dim3(grid1), dim3(kWG), 0, B.stream, B.vol, fr, B.pool,
+                               no_table, B.stats, (const int*)B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         ++B.frames;

@@ -18,7 +18,7 @@
 namespace tsdf {
 
 constexpr int kBrickEdge = 8;
-constexpr int kBrickVox = 512;      // 8^3 voxels; brick-local index = z*64 + x*8 + y
+constexpr int kBrickVox = 512;      // 8^3 voxels; brick-local index = (x*8 + y)*8 + z
 constexpr int kWG = 256;            // threads per workgroup (4 waves of 64)
 constexpr int kPyrLevels = 6;       // max-depth pyramid levels 1..6 (2x2 .. 64x64 pixels)
 constexpr int kStatSpread = 64;     // counters are spread over 64 words (no hot atomic word)
@@ -45,8 +45,10 @@ struct Frame {
     double ow;                // obs_weight as a Python float (f64)
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
-    const void* depth;
-    const void* color;
+    const void* depth;        // the caller's depth (u16 mm or f64 m)
+    const double* depthm;     // f64 metres = NumPy's astype(float)/1000. (k_pyramid writes it)
+    const void* color;        // the caller's colour (RGB8 or folded f32)
+    const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
     int pyr_off[kPyrLevels + 1];
     int pyr_w[kPyrLevels + 1];
@@ -116,17 +118,6 @@ __device__ inline T coh_load(T* p) {
 template <typename T>
 __device__ inline void coh_store(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Depth in metres at pixel p, exactly as NumPy computes it: astype(float) / 1000.
-template <int DK>
-__device__ inline double depth_at(const Frame& fr, int p) {
-    if (DK == 0) {
-        const unsigned short mm = ((const unsigned short*)fr.depth)[p];
-        return (double)mm / 1000.0;
-    } else {
-        return ((const double*)fr.depth)[p];
-    }
 }
 
 // World position of a global voxel index (vox2world, grid_fusion.py:170-181):
@@ -271,11 +262,43 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 
 
 // ---------------------------------------------------------------------------------------------
-// Per-brick integrate: one wave, lane (x,y) = (lane>>3, lane&7) walks z = 0..7, so the
-// x/y part of the camera transform is computed once per column and every z-step's 64 loads
-// and stores are one contiguous 256-B segment of the brick (brick-local index z*64 + lane).
+// Pixel of a camera-space coordinate, exactly as cam2pix (grid_fusion.py:195-196):
+// rint(RN(RN(a / z) + c)) with a = RN(x * f).  Fast path: a reciprocal of z refined to ~1 ulp
+// gives s within ~1e-12 px of the exact sum (|s| < ~1e3, the only range where the pixel can be
+// valid); unless s is within 1e-9 px of a rounding boundary rint(s) is then the exact pixel.
+// Otherwise recompute with the reference's own operation order.
 // ---------------------------------------------------------------------------------------------
-template <bool HASH, int DK, int CK>
+__device__ inline double exact_pixel(double a, double z, double rz, double c) {
+    const double s = a * rz + c;  // -ffp-contract=off: two roundings
+    const double r = rint(s);
+    if (fabs(s - r) < 0.5 - 1e-9 && fabs(s) < 1e9) return r;
+    return rint(a / z + c);
+}
+
+__device__ inline double refined_rcp(double z) {
+    double y = __builtin_amdgcn_rcp(z);
+    double e = fma(-z, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-z, y, 1.0);
+    return fma(y, e, y);
+}
+
+__device__ inline double readlane_f64(double x, int l) {
+    const unsigned long long u = __double_as_longlong(x);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-brick integrate, one wave.  Lane (x,y) = (lane>>3, lane&7) owns the z-column of the brick
+// and walks z = 0..7: the x/y part of the camera transform is computed once per column, and the
+// brick-local layout [x][y][z] makes the column 32 contiguous bytes per field, so the state moves
+// with two 16-byte loads/stores per field per lane (a wave: one contiguous 2 KB segment).  The
+// 8 z-steps go through the phases together (project -> gather depth -> test -> load state and
+// colour -> update -> store) to keep many loads in flight per lane.
+// ---------------------------------------------------------------------------------------------
+template <bool HASH, int CK>
 __device__ inline void integrate_brick(const Vol& v, const Frame& fr, const Pool& pool,
                                        const Table& tab, int b, unsigned long long* s_stat) {
     const int lane = lane_id();
@@ -287,40 +310,52 @@ __device__ inline void integrate_brick(const Vol& v, const Frame& fr, const Pool
     const int lx = bx * kBrickEdge + (lane >> 3);
     const int ly = by * kBrickEdge + (lane & 7);
     const bool col_in = lx < v.dims[0] && ly < v.dims[1];
+    const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge);
     // vox2world + the x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:170-181, 363-368)
     const double px = vox_world(v.origin[0], v.vs, v.off[0] + lx);
     const double py = vox_world(v.origin[1], v.vs, v.off[1] + ly);
     const double a0 = fma(fr.T[1], py, fr.T[0] * px);
     const double a1 = fma(fr.T[5], py, fr.T[4] * px);
     const double a2 = fma(fr.T[9], py, fr.T[8] * px);
+    // the brick's 8 z world coordinates: lanes 0..7 compute them, every lane reads them back
+    const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));
 
-    unsigned vmask = 0;
+    // phase 1: project (grid_fusion.py:262-277)
+    unsigned cand = 0;
     int pix[kBrickEdge];
-    double dist[kBrickEdge];
+    double zc[kBrickEdge];
 #pragma unroll
     for (int k = 0; k < kBrickEdge; ++k) {
         pix[k] = 0;
-        dist[k] = 0.0;
-        const int lz = bz * kBrickEdge + k;
-        if (!col_in || lz >= v.dims[2]) continue;
-        const double pz = vox_world(v.origin[2], v.vs, v.off[2] + lz);
+        const double pz = readlane_f64(pz_l, k);
         const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
-        if (!(z > 0.0)) continue;
+        zc[k] = z;
+        if (!(col_in && k < nz && z > 0.0)) continue;
         const double x = fr.T[3] + fma(fr.T[2], pz, a0);
         const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-        // cam2pix (grid_fusion.py:195-196): mul, div, add, round-half-even
-        const double u = rint((x * fr.fx) / z + fr.cx);
-        const double w = rint((y * fr.fy) / z + fr.cy);
+        const double rz = refined_rcp(z);
+        const double u = exact_pixel(x * fr.fx, z, rz, fr.cx);
+        const double w = exact_pixel(y * fr.fy, z, rz, fr.cy);
         if (!(u >= 0.0 && u < (double)fr.W && w >= 0.0 && w < (double)fr.H)) continue;
-        const int p = (int)w * fr.W + (int)u;
-        // depth test (grid_fusion.py:278-286)
-        const double d = depth_at<DK>(fr, p);
-        const double diff = d - z;
-        if (!(d > 0.0 && diff >= -v.trunc)) continue;
-        const double dd = diff / v.trunc;
-        dist[k] = dd > 1.0 ? 1.0 : dd;  // np.minimum(1, .)
-        pix[k] = p;
-        vmask |= 1u << k;
+        pix[k] = (int)w * fr.W + (int)u;
+        cand |= 1u << k;
+    }
+    // phase 2: gather depth for every candidate at once
+    double dep[kBrickEdge];
+#pragma unroll
+    for (int k = 0; k < kBrickEdge; ++k) dep[k] = ((cand >> k) & 1u) ? fr.depthm[pix[k]] : 0.0;
+    // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
+    unsigned vmask = 0;
+    double dist[kBrickEdge];
+#pragma unroll
+    for (int k = 0; k < kBrickEdge; ++k) {
+        const double diff = dep[k] - zc[k];
+        dist[k] = 0.0;
+        if (((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc) {
+            const double dd = diff / v.trunc;
+            dist[k] = dd > 1.0 ? 1.0 : dd;  // np.minimum(1, .)
+            vmask |= 1u << k;
+        }
     }
     if (__ballot(vmask != 0) == 0) return;
 
@@ -348,50 +383,87 @@ __device__ inline void integrate_brick(const Vol& v, const Frame& fr, const Pool
         }
     }
 
-    const size_t base = (size_t)blk * kBrickVox + lane;
-    int nupd = 0;
+    // phase 4: state (two 16-B halves per field, only halves with a valid voxel) and colour
+    const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge;
+    const bool h0 = (vmask & 0x0Fu) != 0, h1 = (vmask & 0xF0u) != 0;
+    float w_old[kBrickEdge], t_old[kBrickEdge], c_old[kBrickEdge];
 #pragma unroll
     for (int k = 0; k < kBrickEdge; ++k) {
-        const size_t idx = base + (size_t)k * 64;
-        if ((vmask >> k) & 1u) {
-            float w_old = 0.0f, t_old = 1.0f, c_old = 0.0f;
-            if (!(HASH && is_new)) {
-                w_old = pool.weight[idx];
-                t_old = pool.tsdf[idx];
-                c_old = pool.color[idx];
-            }
-            // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average
-            const float w_new = (float)((double)w_old + fr.ow);
-            const float wt = w_old * t_old;
-            const float t_new = (float)(((double)wt + fr.ow * dist[k]) / (double)w_new);
-            // colour (grid_fusion.py:302-314): float32 throughout, round half to even
-            const float ob = floorf(c_old / 65536.0f);
-            const float og = floorf((c_old - ob * 65536.0f) / 256.0f);
-            const float orr = c_old - ob * 65536.0f - og * 256.0f;
-            float nb, ng, nr;
-            if (CK == 0) {  // uint8 RGB: the fold/decode round trip is exact
-                const unsigned char* c = (const unsigned char*)fr.color + 3 * (size_t)pix[k];
-                nr = (float)c[0];
-                ng = (float)c[1];
-                nb = (float)c[2];
-            } else {
-                const float nc = ((const float*)fr.color)[pix[k]];
-                nb = floorf(nc / 65536.0f);
-                ng = floorf((nc - nb * 65536.0f) / 256.0f);
-                nr = nc - nb * 65536.0f - ng * 256.0f;
-            }
-            const float cb = fminf(255.0f, rintf((w_old * ob + fr.ow32 * nb) / w_new));
-            const float cg = fminf(255.0f, rintf((w_old * og + fr.ow32 * ng) / w_new));
-            const float cr = fminf(255.0f, rintf((w_old * orr + fr.ow32 * nr) / w_new));
-            pool.weight[idx] = w_new;
-            pool.tsdf[idx] = t_new;
-            pool.color[idx] = cb * 65536.0f + cg * 256.0f + cr;
-            ++nupd;
-        } else if (HASH && is_new) {  // first touch of a pool block: initialise it
-            pool.weight[idx] = 0.0f;
-            pool.tsdf[idx] = 1.0f;
-            pool.color[idx] = 0.0f;
+        w_old[k] = 0.0f;
+        t_old[k] = 1.0f;
+        c_old[k] = 0.0f;
+    }
+    if (!(HASH && is_new)) {
+        if (h0) {
+            const float4 W = *(const float4*)(pool.weight + base);
+            const float4 T = *(const float4*)(pool.tsdf + base);
+            const float4 C = *(const float4*)(pool.color + base);
+            w_old[0] = W.x; w_old[1] = W.y; w_old[2] = W.z; w_old[3] = W.w;
+            t_old[0] = T.x; t_old[1] = T.y; t_old[2] = T.z; t_old[3] = T.w;
+            c_old[0] = C.x; c_old[1] = C.y; c_old[2] = C.z; c_old[3] = C.w;
         }
+        if (h1) {
+            const float4 W = *(const float4*)(pool.weight + base + 4);
+            const float4 T = *(const float4*)(pool.tsdf + base + 4);
+            const float4 C = *(const float4*)(pool.color + base + 4);
+            w_old[4] = W.x; w_old[5] = W.y; w_old[6] = W.z; w_old[7] = W.w;
+            t_old[4] = T.x; t_old[5] = T.y; t_old[6] = T.z; t_old[7] = T.w;
+            c_old[4] = C.x; c_old[5] = C.y; c_old[6] = C.z; c_old[7] = C.w;
+        }
+    }
+    unsigned cpx[kBrickEdge];
+#pragma unroll
+    for (int k = 0; k < kBrickEdge; ++k) {
+        cpx[k] = 0u;
+        if ((vmask >> k) & 1u) cpx[k] = (CK == 0) ? fr.rgbx[pix[k]] : __float_as_uint(((const float*)fr.color)[pix[k]]);
+    }
+    // phase 5: update
+    int nupd = 0;
+    float w_new[kBrickEdge], t_new[kBrickEdge], c_new[kBrickEdge];
+#pragma unroll
+    for (int k = 0; k < kBrickEdge; ++k) {
+        w_new[k] = w_old[k];
+        t_new[k] = t_old[k];
+        c_new[k] = c_old[k];
+        if (!((vmask >> k) & 1u)) continue;
+        // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average
+        const float wn = (float)((double)w_old[k] + fr.ow);
+        const float wt = w_old[k] * t_old[k];
+        t_new[k] = (float)(((double)wt + fr.ow * dist[k]) / (double)wn);
+        w_new[k] = wn;
+        // colour (grid_fusion.py:302-314): float32 throughout, round half to even
+        float nb, ng, nr;
+        if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
+            nr = (float)(cpx[k] & 0xFFu);
+            ng = (float)((cpx[k] >> 8) & 0xFFu);
+            nb = (float)((cpx[k] >> 16) & 0xFFu);
+        } else {
+            const float nc = __uint_as_float(cpx[k]);
+            nb = floorf(nc / 65536.0f);
+            ng = floorf((nc - nb * 65536.0f) / 256.0f);
+            nr = nc - nb * 65536.0f - ng * 256.0f;
+        }
+        const float co = c_old[k];
+        const float ob = floorf(co / 65536.0f);
+        const float og = floorf((co - ob * 65536.0f) / 256.0f);
+        const float orr = co - ob * 65536.0f - og * 256.0f;
+        const float cb = fminf(255.0f, rintf((w_old[k] * ob + fr.ow32 * nb) / wn));
+        const float cg = fminf(255.0f, rintf((w_old[k] * og + fr.ow32 * ng) / wn));
+        const float cr = fminf(255.0f, rintf((w_old[k] * orr + fr.ow32 * nr) / wn));
+        c_new[k] = cb * 65536.0f + cg * 256.0f + cr;
+        ++nupd;
+    }
+    // phase 6: store the halves that changed (a new hash block is written whole: its init)
+    const bool s0 = h0 || (HASH && is_new), s1 = h1 || (HASH && is_new);
+    if (s0) {
+        *(float4*)(pool.weight + base) = make_float4(w_new[0], w_new[1], w_new[2], w_new[3]);
+        *(float4*)(pool.tsdf + base) = make_float4(t_new[0], t_new[1], t_new[2], t_new[3]);
+        *(float4*)(pool.color + base) = make_float4(c_new[0], c_new[1], c_new[2], c_new[3]);
+    }
+    if (s1) {
+        *(float4*)(pool.weight + base + 4) = make_float4(w_new[4], w_new[5], w_new[6], w_new[7]);
+        *(float4*)(pool.tsdf + base + 4) = make_float4(t_new[4], t_new[5], t_new[6], t_new[7]);
+        *(float4*)(pool.color + base + 4) = make_float4(c_new[4], c_new[5], c_new[6], c_new[7]);
     }
     if (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns the block this launch
         unsigned long long mine = 0;
@@ -414,59 +486,8 @@ __device__ inline void integrate_brick(const Vol& v, const Frame& fr, const Pool
     }
 }
 
-// Fused cull + integrate.  Workgroup g owns bricks {g + t*G : t < 256} (G = gridDim.x): an
-// interleaved sample of the whole volume, so every workgroup gets a similar share of the
-// visible bricks without a global work queue.  With `list` the bricks come from it instead
-// (hash overflow re-run).
-template <bool HASH, int DK, int CK>
-__global__ __launch_bounds__(kWG) void k_integrate(Vol v, Frame fr, Pool pool, Table tab,
-                                                  unsigned long long* stats, const int* list,
-                                                  int n_list) {
-    __shared__ int s_list[kWG];
-    __shared__ int s_cnt[kWG / 64];
-    __shared__ unsigned long long s_stat[kNStat];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid < kNStat) s_stat[tid] = 0;
-    bool keep = false;
-    int b = 0;
-    if (list) {
-        const long long e = (long long)blockIdx.x * kWG + tid;
-        if (e < n_list) {
-            b = list[e];
-            keep = true;
-        }
-    } else {
-        const long long nbricks = (long long)v.nb[0] * v.nb[1] * v.nb[2];
-        const long long e = (long long)blockIdx.x + (long long)tid * gridDim.x;
-        if (e < nbricks) {
-            b = (int)e;
-            const int nb12 = v.nb[1] * v.nb[2];
-            const int bx = b / nb12, rem = b - bx * nb12, by = rem / v.nb[2], bz = rem - by * v.nb[2];
-            keep = true;
-            if (HASH && v.n_shards > 1) {  // bucket-range ownership
-                const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
-                keep = (int)((home * v.n_shards) / tab.capacity) == v.shard;
-            }
-            if (keep) keep = cull_brick(v, fr, bx, by, bz);
-        }
-    }
-    // compact the survivors: wave ballot + LDS prefix over the 4 waves
-    const unsigned long long m = __ballot(keep);
-    if (lane == 0) s_cnt[wave] = __popcll(m);
-    __syncthreads();
-    int base = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kWG / 64; ++w) {
-        const int c = s_cnt[w];
-        base += (w < wave) ? c : 0;
-        total += c;
-    }
-    if (keep) s_list[base + __popcll(m & ((1ull << lane) - 1ull))] = b;
-    __syncthreads();
-    for (int e = wave; e < total; e += kWG / 64)
-        integrate_brick<HASH, DK, CK>(v, fr, pool, tab, s_list[e], s_stat);
-    if (tid == 0) atomicAdd(&s_stat[ST_VISITED], (unsigned long long)total);
-    __syncthreads();
+__device__ inline void flush_stats(unsigned long long* s_stat, unsigned long long* stats) {
+    const int tid = threadIdx.x;
     if (tid < kNStat && s_stat[tid]) {
         unsigned long long* dst = stats + tid * kStatSpread + (blockIdx.x & (kStatSpread - 1));
         if (tid == ST_PROBE_MAX) atomicMax(dst, s_stat[tid]);
@@ -474,74 +495,130 @@ __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Frame fr, Pool pool, T
     }
 }
 
-// Max-depth pyramid, levels 1..6 (texel = max over a 2^L x 2^L pixel block, metres, 0 for
-// invalid/outside).  One workgroup per 64x64 tile; each thread reduces a 4x4 patch.
-template <int DK>
-__global__ __launch_bounds__(kWG) void k_pyramid(Frame fr, float* pyr) {
-    __shared__ float s2[16][16];
-    __shared__ float s3[8][8];
-    __shared__ float s4[4][4];
-    __shared__ float s5[2][2];
-    const int t = threadIdx.x, r = t >> 4, c = t & 15;
-    const int x0 = blockIdx.x * 64 + c * 4, y0 = blockIdx.y * 64 + r * 4;
-    float m2 = 0.0f;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            float m1 = 0.0f;
-#pragma unroll
-            for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < 2; ++dx) {
-                    const int x = x0 + q * 2 + dx, y = y0 + a * 2 + dy;
-                    if (x < fr.W && y < fr.H) {
-                        const int p = y * fr.W + x;
-                        const float d = (DK == 0) ? (float)((const unsigned short*)fr.depth)[p] * 1e-3f
-                                                  : (float)((const double*)fr.depth)[p];
-                        m1 = fmaxf(m1, d);
-                    }
-                }
-            const int tx1 = (x0 >> 1) + q, ty1 = (y0 >> 1) + a;
-            if (tx1 < fr.pyr_w[1] && ty1 < fr.pyr_h[1]) pyr[fr.pyr_off[1] + ty1 * fr.pyr_w[1] + tx1] = m1;
-            m2 = fmaxf(m2, m1);
+// Conservative cull of every brick (one lane each) and compaction of the survivors into a
+// frame-wide list: wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
+template <bool HASH>
+__global__ __launch_bounds__(kWG) void k_cull(Vol v, Frame fr, Table tab, int* list,
+                                             unsigned int* count, unsigned long long* stats) {
+    __shared__ int s_cnt[kWG / 64];
+    __shared__ unsigned int s_base;
+    __shared__ unsigned long long s_stat[kNStat];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < kNStat) s_stat[tid] = 0;
+    const long long nbricks = (long long)v.nb[0] * v.nb[1] * v.nb[2];
+    const long long e = (long long)blockIdx.x * kWG + tid;
+    bool keep = false;
+    if (e < nbricks) {
+        const int b = (int)e;
+        const int nb12 = v.nb[1] * v.nb[2];
+        const int bx = b / nb12, rem = b - bx * nb12, by = rem / v.nb[2], bz = rem - by * v.nb[2];
+        keep = true;
+        if (HASH && v.n_shards > 1) {  // bucket-range ownership
+            const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
+            keep = (int)((home * v.n_shards) / tab.capacity) == v.shard;
         }
-    if ((x0 >> 2) < fr.pyr_w[2] && (y0 >> 2) < fr.pyr_h[2])
-        pyr[fr.pyr_off[2] + (y0 >> 2) * fr.pyr_w[2] + (x0 >> 2)] = m2;
-    s2[r][c] = m2;
+        if (keep) keep = cull_brick(v, fr, bx, by, bz);
+    }
+    const unsigned long long m = __ballot(keep);
+    if (lane == 0) s_cnt[wave] = __popcll(m);
     __syncthreads();
-    if (t < 64) {
-        const int rr = t >> 3, cc = t & 7;
-        const float m = fmaxf(fmaxf(s2[2 * rr][2 * cc], s2[2 * rr][2 * cc + 1]),
-                              fmaxf(s2[2 * rr + 1][2 * cc], s2[2 * rr + 1][2 * cc + 1]));
-        s3[rr][cc] = m;
-        const int X = blockIdx.x * 8 + cc, Y = blockIdx.y * 8 + rr;
-        if (X < fr.pyr_w[3] && Y < fr.pyr_h[3]) pyr[fr.pyr_off[3] + Y * fr.pyr_w[3] + X] = m;
+    if (tid == 0) {
+        int tot = 0;
+        for (int w = 0; w < kWG / 64; ++w) tot += s_cnt[w];
+        s_base = tot ? atomicAdd(count, (unsigned)tot) : 0u;
+        s_stat[ST_VISITED] = (unsigned long long)tot;
     }
     __syncthreads();
-    if (t < 16) {
-        const int rr = t >> 2, cc = t & 3;
-        const float m = fmaxf(fmaxf(s3[2 * rr][2 * cc], s3[2 * rr][2 * cc + 1]),
-                              fmaxf(s3[2 * rr + 1][2 * cc], s3[2 * rr + 1][2 * cc + 1]));
-        s4[rr][cc] = m;
-        const int X = blockIdx.x * 4 + cc, Y = blockIdx.y * 4 + rr;
-        if (X < fr.pyr_w[4] && Y < fr.pyr_h[4]) pyr[fr.pyr_off[4] + Y * fr.pyr_w[4] + X] = m;
-    }
+    int off = 0;
+#pragma unroll
+    for (int w = 0; w < kWG / 64; ++w) off += (w < wave) ? s_cnt[w] : 0;
+    if (keep) list[s_base + off + __popcll(m & ((1ull << lane) - 1ull))] = (int)e;
+    flush_stats(s_stat, stats);
+}
+
+// Integrate the listed bricks: each wave takes list entries gw, gw + NW, ... (NW = waves in the
+// grid), so the work is spread evenly whatever the frame sees.  `count` (device) gives the list
+// length written by k_cull; with count == nullptr the first n_list entries are used (hash
+// overflow re-run).
+template <bool HASH, int CK>
+__global__ __launch_bounds__(kWG) void k_integrate(Vol v, Frame fr, Pool pool, Table tab,
+                                                  unsigned long long* stats, const int* list,
+                                                  unsigned int* count, int n_list) {
+    __shared__ unsigned long long s_stat[kNStat];
+    const int tid = threadIdx.x;
+    if (tid < kNStat) s_stat[tid] = 0;
     __syncthreads();
-    if (t < 4) {
-        const int rr = t >> 1, cc = t & 1;
-        const float m = fmaxf(fmaxf(s4[2 * rr][2 * cc], s4[2 * rr][2 * cc + 1]),
-                              fmaxf(s4[2 * rr + 1][2 * cc], s4[2 * rr + 1][2 * cc + 1]));
-        s5[rr][cc] = m;
-        const int X = blockIdx.x * 2 + cc, Y = blockIdx.y * 2 + rr;
-        if (X < fr.pyr_w[5] && Y < fr.pyr_h[5]) pyr[fr.pyr_off[5] + Y * fr.pyr_w[5] + X] = m;
-    }
+    const int n = count ? (int)coh_load(count) : n_list;
+    const int nw = gridDim.x * (kWG / 64);
+    for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
+        integrate_brick<HASH, CK>(v, fr, pool, tab, list[e], s_stat);
     __syncthreads();
-    if (t == 0) {
-        const float m = fmaxf(fmaxf(s5[0][0], s5[0][1]), fmaxf(s5[1][0], s5[1][1]));
-        const int X = blockIdx.x, Y = blockIdx.y;
-        if (X < fr.pyr_w[6] && Y < fr.pyr_h[6]) pyr[fr.pyr_off[6] + Y * fr.pyr_w[6] + X] = m;
+    flush_stats(s_stat, stats);
+}
+
+// Per frame, before the cull (one pass over the image): the f64 metres image (u16 input, exactly
+// NumPy's astype(float)/1000.), the packed RGB8 image, the max-depth pyramid levels 1..6
+// (texel = max over a 2^L x 2^L block, metres, 0 for invalid/outside) and the reset of the
+// brick-list counter.  One 1024-thread workgroup per 64x64 tile, 2x2 pixels per thread.
+template <int REDUCE>
+__device__ inline void pyr_level(const Frame& fr, float* pyr, int L, const float (*src)[33],
+                                 float (*dst)[33], int n) {
+    const int t = threadIdx.x;
+    if (t < n * n) {
+        const int rr = t / n, cc = t - rr * n;
+        const float m = fmaxf(fmaxf(src[2 * rr][2 * cc], src[2 * rr][2 * cc + 1]),
+                              fmaxf(src[2 * rr + 1][2 * cc], src[2 * rr + 1][2 * cc + 1]));
+        dst[rr][cc] = m;
+        const int X = blockIdx.x * n + cc, Y = blockIdx.y * n + rr;
+        if (X < fr.pyr_w[L] && Y < fr.pyr_h[L]) pyr[fr.pyr_off[L] + Y * fr.pyr_w[L] + X] = m;
     }
+}
+
+template <int DK, int CK>
+__global__ __launch_bounds__(1024) void k_prep(Frame fr, float* pyr, double* depthm, unsigned* rgbx,
+                                              unsigned int* count) {
+    __shared__ float sa[32][33];
+    __shared__ float sb[32][33];
+    const int t = threadIdx.x, r = t >> 5, c = t & 31;
+    if (count && t == 0 && blockIdx.x == 0 && blockIdx.y == 0) coh_store(count, 0u);
+    const int x0 = blockIdx.x * 64 + c * 2, y0 = blockIdx.y * 64 + r * 2;
+    float m1 = 0.0f;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+            const int x = x0 + dx, y = y0 + dy;
+            if (x < fr.W && y < fr.H) {
+                const int p = y * fr.W + x;
+                double d;
+                if (DK == 0) {  // NumPy: depth.astype(float) / 1000. (grid_demo1.py:81-82)
+                    d = (double)((const unsigned short*)fr.depth)[p] / 1000.0;
+                    depthm[p] = d;
+                } else {
+                    d = ((const double*)fr.depth)[p];
+                }
+                if (CK == 0) {
+                    const unsigned char* q = (const unsigned char*)fr.color + 3 * (size_t)p;
+                    rgbx[p] = (unsigned)q[0] | ((unsigned)q[1] << 8) | ((unsigned)q[2] << 16);
+                }
+                m1 = fmaxf(m1, (float)d);
+            }
+        }
+    {
+        const int X = (x0 >> 1), Y = (y0 >> 1);
+        if (X < fr.pyr_w[1] && Y < fr.pyr_h[1]) pyr[fr.pyr_off[1] + Y * fr.pyr_w[1] + X] = m1;
+    }
+    sa[r][c] = m1;
+    __syncthreads();
+    pyr_level<0>(fr, pyr, 2, sa, sb, 16);
+    __syncthreads();
+    pyr_level<0>(fr, pyr, 3, sb, sa, 8);
+    __syncthreads();
+    pyr_level<0>(fr, pyr, 4, sa, sb, 4);
+    __syncthreads();
+    pyr_level<0>(fr, pyr, 5, sb, sa, 2);
+    __syncthreads();
+    pyr_level<0>(fr, pyr, 6, sa, sb, 1);
 }
 
 }  // namespace tsdf

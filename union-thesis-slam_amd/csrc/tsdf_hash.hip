@@ -65,7 +65,7 @@ __device__ bool voxel_brick(const Vol& v, long long x, long long y, long long z,
     *bx = (int)(x >> 3);
     *by = (int)(y >> 3);
     *bz = (int)(z >> 3);
-    *local = (int)((z & 7) * 64 + (x & 7) * 8 + (y & 7));
+    *local = (int)(((x & 7) * 8 + (y & 7)) * 8 + (z & 7));  // pool index; entry bit: word z, bit x*8+y
     return true;
 }
 
@@ -80,8 +80,8 @@ __global__ void k_lookup(Vol v, Table t, Pool pool, const long long* ijk, long l
         const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
         if (s >= 0) {
             const long long blk = coh_load(&t.vals[s]);
-            const unsigned long long word = coh_load(&t.occ[blk * 8 + (local >> 6)]);
-            if ((word >> (local & 63)) & 1ull) {
+            const unsigned long long word = coh_load(&t.occ[blk * 8 + (local & 7)]);
+            if ((word >> (local >> 3)) & 1ull) {
                 f = 1;
                 const size_t j = (size_t)blk * kBrickVox + local;
                 tv = coh_load(&pool.tsdf[j]);
@@ -152,7 +152,7 @@ __global__ void k_set_voxels(Vol v, Table t, Pool pool, const long long* ijk, lo
     const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
     if (s < 0) return;
     const long long blk = coh_load(&t.vals[s]);
-    atomicOr(&t.occ[blk * 8 + (local >> 6)], 1ull << (local & 63));
+    atomicOr(&t.occ[blk * 8 + (local & 7)], 1ull << (local >> 3));
     const size_t j = (size_t)blk * kBrickVox + local;
     if (it) pool.tsdf[j] = it[i];
     if (iw) pool.weight[j] = iw[i];
@@ -169,8 +169,8 @@ __global__ void k_remove_voxels(Vol v, Table t, const long long* ijk, long long 
         const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
         if (s >= 0) {
             const long long blk = coh_load(&t.vals[s]);
-            const unsigned long long bit = 1ull << (local & 63);
-            const unsigned long long old = atomicAnd(&t.occ[blk * 8 + (local >> 6)], ~bit);
+            const unsigned long long bit = 1ull << (local >> 3);
+            const unsigned long long old = atomicAnd(&t.occ[blk * 8 + (local & 7)], ~bit);
             r = (old & bit) ? 1 : 0;
         }
     }
@@ -251,7 +251,7 @@ __global__ void k_to_dense(Vol v, Table t, Pool pool, float* ot, float* ow, floa
             const int x = bx * 8 + (bit >> 3), y = by * 8 + (bit & 7), z = bz * 8 + kz;
             if (x >= v.dims[0] || y >= v.dims[1] || z >= v.dims[2]) continue;
             const size_t o = ((size_t)x * v.dims[1] + y) * v.dims[2] + z;
-            const size_t j = (size_t)blk * kBrickVox + kz * 64 + bit;
+            const size_t j = (size_t)blk * kBrickVox + bit * 8 + kz;
             if (ot) ot[o] = coh_load(&pool.tsdf[j]);
             if (ow) ow[o] = coh_load(&pool.weight[j]);
             if (oc) oc[o] = coh_load(&pool.color[j]);
@@ -355,33 +355,37 @@ int ensure_room(tsdf_hash* h) {
     return TSDF_OK;
 }
 
-template <bool HASH>
-void launch_integrate(tsdf_hash* h, const Frame& fr, int dk, int ck, unsigned grid, const int* list, int n_list) {
+// One hash integrate pass: the listed bricks (list/count from k_cull, or an explicit list).
+void launch_integrate(tsdf_hash* h, const Frame& fr, int ck, const int* list, unsigned int* count,
+                      int n_list) {
     Base& B = h->b;
-    if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_integrate<true, 0, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
-    else if (dk == TSDF_DEPTH_U16_MM)
-        hipLaunchKernelGGL((k_integrate<true, 0, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
-    else if (ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_integrate<true, 1, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
+    const void* kern = ck == TSDF_COLOR_RGB8 ? (const void*)k_integrate<true, 0> : (const void*)k_integrate<true, 1>;
+    const unsigned grid = B.grid_for(kern);
+    if (ck == TSDF_COLOR_RGB8)
+        hipLaunchKernelGGL((k_integrate<true, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t,
+                           B.stats, list, count, n_list);
     else
-        hipLaunchKernelGGL((k_integrate<true, 1, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t, B.stats, list, n_list);
+        hipLaunchKernelGGL((k_integrate<true, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t,
+                           B.stats, list, count, n_list);
 }
 
 int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int ck,
              int H, int W, const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
-    const unsigned grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
     const bool sync_each = !(flags & TSDF_ASYNC) && n_frames == 1;
     for (int f = 0; f < n_frames; ++f) {
         Frame fr;
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
         TSDF_TRY(B.prepare_frame(&fr, depth, dk, color, ck, H, W, K, Tinv + 16 * (size_t)f, 1.0, flags, f));
-        TSDF_TRY(B.launch_pyramid(fr, dk));
+        TSDF_TRY(B.launch_prep(fr, dk, ck));
+        hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, fr, h->t, B.list,
+                           B.count, B.stats);
+        TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
-        launch_integrate<true>(h, fr, dk, ck, grid, nullptr, 0);
+        launch_integrate(h, fr, ck, (const int*)B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
@@ -409,7 +413,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
                 TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
             else
                 TSDF_TRY(resize_table(h, h->t.capacity * 2));
-            launch_integrate<true>(h, fr, dk, ck, (unsigned)((n_ov + kWG - 1) / kWG), h->d_list, (int)n_ov);
+            launch_integrate(h, fr, ck, h->d_list, nullptr, (int)n_ov);
             TSDF_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
             TSDF_HIP(hipGetLastError());
@@ -646,7 +650,7 @@ int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float*
             const unsigned long long k = pack_key((int)(x >> 3), (int)(y >> 3), (int)(z >> 3));
             const long long j = std::lower_bound(keys.begin(), keys.end(), k) - keys.begin();
             if (slot) slot[i] = sl[j];
-            if (local) local[i] = (int32_t)((z & 7) * 64 + (x & 7) * 8 + (y & 7));
+            if (local) local[i] = (int32_t)(((x & 7) * 8 + (y & 7)) * 8 + (z & 7));
         }
     }
     return TSDF_OK;

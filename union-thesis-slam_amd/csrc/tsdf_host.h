@@ -59,7 +59,12 @@ struct Base {
     Pool pool{};
     long long n_bricks = 0;
     float* pyr = nullptr;
+    double* depthm = nullptr;  // per-frame f64 metres image (u16 input)
+    unsigned* rgbx = nullptr;  // per-frame packed RGB8 image
     int pyr_H = 0, pyr_W = 0;
+    int* list = nullptr;        // per-frame list of bricks that survive the cull
+    unsigned int* count = nullptr;
+    int n_cu = 256;             // compute units of the device
     PyrLayout lay{};
     unsigned long long* stats = nullptr;  // kNStat x kStatSpread
     long long frames = 0;
@@ -77,7 +82,10 @@ struct Base {
     int prepare_frame(Frame* fr, const void* depth, int dk, const void* color, int ck, int H,
                       int W, const double K[9], const double Tinv[16], double ow, int flags,
                       int frame_index);
-    int launch_pyramid(const Frame& fr, int dk);
+    int launch_prep(const Frame& fr, int dk, int ck);
+    // Workgroups of the integrate kernel: as many as can be resident (occupancy x CUs), capped
+    // by the work there can be (4 bricks per workgroup per round).
+    unsigned grid_for(const void* kernel);
     int read_stats(tsdf_stats_t* out, int reset);
     int set_profiling(int on);
     void release();

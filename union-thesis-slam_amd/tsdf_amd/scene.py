@@ -84,10 +84,12 @@ def trajectory(n_frames: int, seed: int = 0, room: float = ROOM, start: int = 0,
 
 
 def render(poses, spheres: np.ndarray, room: float = ROOM, seed: int = 0, start: int = 0,
-           invalid_frac: float = 0.05, device="cpu", h: int = H, w: int = W):
+           invalid_frac: float = 0.05, device="cpu", h: int = H, w: int = W, depth_dtype=None):
     """Ray-cast frames.  Returns torch tensors on `device`:
-    depth (F,H,W) uint16 millimetres (0 = invalid), rgb (F,H,W,3) uint8 (RGB order, like
-    `cv2.cvtColor(..., COLOR_BGR2RGB)` in the reference demos).
+    depth (F,H,W) millimetres (0 = invalid) as uint16 -- or, with depth_dtype=torch.int16, the
+    same bits as int16 (every depth here is < 32.768 m), which is what the GPU path keeps in
+    HBM since torch's uint16 support on the device is partial; rgb (F,H,W,3) uint8 (RGB order,
+    like `cv2.cvtColor(..., COLOR_BGR2RGB)` in the reference demos).
     """
     import torch
 
@@ -126,7 +128,7 @@ def render(poses, spheres: np.ndarray, room: float = ROOM, seed: int = 0, start:
         rgb[f, ..., 0] = ((hsh >> 3) & 255).to(torch.uint8)
         rgb[f, ..., 1] = ((hsh >> 11) & 255).to(torch.uint8)
         rgb[f, ..., 2] = ((hsh >> 19) & 255).to(torch.uint8)
-    return depth.to(torch.uint16), rgb
+    return depth.to(depth_dtype or torch.uint16), rgb
 
 
 def depth_metres(depth_u16: np.ndarray) -> np.ndarray:
