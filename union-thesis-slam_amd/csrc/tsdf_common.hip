@@ -113,10 +113,10 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     vol.shard = 0;
     vol.n_shards = 1;
     n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];
-    if (n_bricks >= (1ll << 31)) return set_error(TSDF_E_ARG, "too many bricks");
+    if (n_bricks >= (1ll << 24)) return set_error(TSDF_E_ARG, "too many bricks (%lld >= 2^24)", n_bricks);
     TSDF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    TSDF_HIP(hipMalloc(&list, sizeof(int) * (size_t)n_bricks));
+    TSDF_HIP(hipMalloc(&list, sizeof(unsigned) * (size_t)n_bricks));
     TSDF_HIP(hipMalloc(&count, sizeof(unsigned int) * 4));
     TSDF_HIP(hipMemsetAsync(count, 0, sizeof(unsigned int) * 4, stream));
     TSDF_HIP(hipMalloc(&stats, sizeof(unsigned long long) * kNStat * kStatSpread));
@@ -136,9 +136,9 @@ int Base::ensure_pyr(int H, int W) {
         rgbx = nullptr;
     }
     lay = pyr_layout(H, W);
-    TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total));
-    TSDF_HIP(hipMalloc(&depthm, sizeof(double) * (size_t)H * W));
-    TSDF_HIP(hipMalloc(&rgbx, sizeof(unsigned) * (size_t)H * W));
+    TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total * kMaxBatch));
+    TSDF_HIP(hipMalloc(&depthm, sizeof(double) * (size_t)H * W * kMaxBatch));
+    TSDF_HIP(hipMalloc(&rgbx, sizeof(unsigned) * (size_t)H * W * kMaxBatch));
     pyr_H = H;
     pyr_W = W;
     return TSDF_OK;
@@ -154,65 +154,70 @@ int check_frame_args(const void* depth, int dk, const void* color, int ck, int H
     return TSDF_OK;
 }
 
-int Base::prepare_frame(Frame* fr, const void* depth, int dk, const void* color, int ck, int H,
-                        int W, const double K[9], const double Tinv[16], double ow, int flags,
-                        int frame_index) {
+int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
+                        int W, const double K[9], const double* Tinv, const double* ow,
+                        double ow_default, int flags, int first, int n) {
     TSDF_TRY(ensure_pyr(H, W));
     const size_t npx = (size_t)H * W;
     const size_t dbytes = npx * (dk == TSDF_DEPTH_U16_MM ? 2 : 8);
     const size_t cbytes = npx * (ck == TSDF_COLOR_RGB8 ? 3 : 4);
-    const char* d = (const char*)depth + dbytes * (size_t)frame_index;
-    const char* c = (const char*)color + cbytes * (size_t)frame_index;
-    if (!(flags & TSDF_DEVICE_PTRS)) {
-        if (st_depth_bytes < dbytes) {
+    const char* d = (const char*)depth + dbytes * (size_t)first;
+    const char* c = (const char*)color + cbytes * (size_t)first;
+    if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames (pageable host memory)
+        if (st_depth_bytes < dbytes * kMaxBatch) {
             TSDF_HIP(hipStreamSynchronize(stream));
             if (st_depth) TSDF_HIP(hipFree(st_depth));
-            TSDF_HIP(hipMalloc(&st_depth, dbytes));
-            st_depth_bytes = dbytes;
+            TSDF_HIP(hipMalloc(&st_depth, dbytes * kMaxBatch));
+            st_depth_bytes = dbytes * kMaxBatch;
         }
-        if (st_color_bytes < cbytes) {
+        if (st_color_bytes < cbytes * kMaxBatch) {
             TSDF_HIP(hipStreamSynchronize(stream));
             if (st_color) TSDF_HIP(hipFree(st_color));
-            TSDF_HIP(hipMalloc(&st_color, cbytes));
-            st_color_bytes = cbytes;
+            TSDF_HIP(hipMalloc(&st_color, cbytes * kMaxBatch));
+            st_color_bytes = cbytes * kMaxBatch;
         }
-        TSDF_HIP(hipMemcpyAsync(st_depth, d, dbytes, hipMemcpyHostToDevice, stream));
-        TSDF_HIP(hipMemcpyAsync(st_color, c, cbytes, hipMemcpyHostToDevice, stream));
+        TSDF_HIP(hipMemcpyAsync(st_depth, d, dbytes * n, hipMemcpyHostToDevice, stream));
+        TSDF_HIP(hipMemcpyAsync(st_color, c, cbytes * n, hipMemcpyHostToDevice, stream));
         d = (const char*)st_depth;
         c = (const char*)st_color;
     }
-    for (int r = 0; r < 12; ++r) fr->T[r] = Tinv[r];
-    fr->fx = (double)(float)K[0];
-    fr->fy = (double)(float)K[4];
-    fr->cx = (double)(float)K[2];
-    fr->cy = (double)(float)K[5];
-    fr->ow = ow;
-    fr->ow32 = (float)ow;
-    fr->H = H;
-    fr->W = W;
-    fr->depth = d;
-    fr->depthm = dk == TSDF_DEPTH_U16_MM ? depthm : (const double*)d;
-    fr->color = c;
-    fr->rgbx = rgbx;
-    fr->pyr = pyr;
-    for (int L = 0; L <= kPyrLevels; ++L) {
-        fr->pyr_off[L] = lay.off[L];
-        fr->pyr_w[L] = lay.w[L];
-        fr->pyr_h[L] = lay.h[L];
+    bt->n = n;
+    for (int i = 0; i < n; ++i) {
+        Frame* fr = &bt->f[i];
+        const double* T = Tinv + 16 * (size_t)(first + i);
+        for (int r = 0; r < 12; ++r) fr->T[r] = T[r];
+        fr->fx = (double)(float)K[0];
+        fr->fy = (double)(float)K[4];
+        fr->cx = (double)(float)K[2];
+        fr->cy = (double)(float)K[5];
+        fr->ow = ow ? ow[first + i] : ow_default;
+        fr->ow32 = (float)fr->ow;
+        fr->H = H;
+        fr->W = W;
+        fr->depth = d + dbytes * i;
+        fr->depthm = dk == TSDF_DEPTH_U16_MM ? depthm + npx * i : (const double*)(d + dbytes * i);
+        fr->color = c + cbytes * i;
+        fr->rgbx = rgbx + npx * i;
+        fr->pyr = pyr + (size_t)lay.total * i;
+        for (int L = 0; L <= kPyrLevels; ++L) {
+            fr->pyr_off[L] = lay.off[L];
+            fr->pyr_w[L] = lay.w[L];
+            fr->pyr_h[L] = lay.h[L];
+        }
     }
     return TSDF_OK;
 }
 
-int Base::launch_prep(const Frame& fr, int dk, int ck) {
-    dim3 grid((fr.W + 63) / 64, (fr.H + 63) / 64);
+int Base::launch_prep(const Batch& bt, int dk, int ck, int W, int H) {
+    dim3 grid((W + 63) / 64, (H + 63) / 64, bt.n);
     if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_prep<0, 0>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
+        hipLaunchKernelGGL((k_prep<0, 0>), grid, dim3(1024), 0, stream, bt, count);
     else if (dk == TSDF_DEPTH_U16_MM)
-        hipLaunchKernelGGL((k_prep<0, 1>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
+        hipLaunchKernelGGL((k_prep<0, 1>), grid, dim3(1024), 0, stream, bt, count);
     else if (ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_prep<1, 0>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
+        hipLaunchKernelGGL((k_prep<1, 0>), grid, dim3(1024), 0, stream, bt, count);
     else
-        hipLaunchKernelGGL((k_prep<1, 1>), grid, dim3(1024), 0, stream, fr, pyr, depthm, rgbx, count);
+        hipLaunchKernelGGL((k_prep<1, 1>), grid, dim3(1024), 0, stream, bt, count);
     TSDF_HIP(hipGetLastError());
     return TSDF_OK;
 }

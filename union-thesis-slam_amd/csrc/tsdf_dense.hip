@@ -47,25 +47,25 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
     const unsigned grid0 = B.grid_for((const void*)k_integrate<false, 0>);
     const unsigned grid1 = B.grid_for((const void*)k_integrate<false, 1>);
-    for (int f = 0; f < n_frames; ++f) {
-        Frame fr;
-        TSDF_TRY(B.prepare_frame(&fr, depth, dk, color, ck, H, W, K, Tinv + 16 * (size_t)f,
-                                 ow ? ow[f] : 1.0, flags, f));
-        TSDF_TRY(B.launch_prep(fr, dk, ck));
-        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, fr, no_table,
+    for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
+        Batch bt;
+        const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+        TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, ow, 1.0, flags, f0, n));
+        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H));
+        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, bt, no_table,
                            B.list, B.count, B.stats);
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
         if (ck == TSDF_COLOR_RGB8)
-            hipLaunchKernelGGL((k_integrate<false, 0>), dim3(grid0), dim3(kWG), 0, B.stream, B.vol, fr, B.pool,
-                               no_table, B.stats, (const int*)B.list, B.count, 0);
+            hipLaunchKernelGGL((k_integrate<false, 0>), dim3(grid0), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
+                               no_table, B.stats, (const unsigned*)B.list, B.count, 0);
         else
-            hipLaunchKernelGGL((k_integrate<false, 1>), dim3(grid1), dim3(kWG), 0, B.stream, B.vol, fr, B.pool,
-                               no_table, B.stats, (const int*)B.list, B.count, 0);
+            hipLaunchKernelGGL((k_integrate<false, 1>), dim3(grid1), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
+                               no_table, B.stats, (const unsigned*)B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
-        ++B.frames;
+        B.frames += n;
     }
     if (!(flags & TSDF_ASYNC)) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;

@@ -55,6 +55,15 @@ struct Frame {
     int pyr_h[kPyrLevels + 1];
 };
 
+// Up to kMaxBatch consecutive frames integrated by one launch (temporal batching: each voxel's
+// updates are still applied frame by frame, in order, so results are those of one-by-one
+// integration; the brick state is read and written once per batch instead of once per frame).
+constexpr int kMaxBatch = 8;
+struct Batch {
+    Frame f[kMaxBatch];
+    int n;
+};
+
 // Brick storage: SoA pool of 512-voxel bricks.
 struct Pool {
     float* tsdf;
@@ -75,7 +84,7 @@ struct Table {
     int* vals;                  // pool block of each slot
     unsigned long long* occ;    // [max_blocks][8] voxel-entry bits (word = z, bit = x*8+y)
     int* free_list;
-    int* overflow;              // brick ids skipped this launch
+    int* overflow;              // list entries (brick | frame mask << 24) skipped this launch
     PoolState* st;
     long long capacity;
     long long max_blocks;
@@ -126,53 +135,72 @@ __device__ inline double vox_world(float origin, double vs, int g) {
     return (double)(float)((double)origin + vs * (double)g);
 }
 
-// Conservative cull of one brick against the frame.  True = some voxel of the brick MAY pass
-// the reference's masks (grid_fusion.py:273-290).  Never drops a brick that has a valid voxel:
-// the box of voxel centres is projected exactly (f64), its pixel bbox grown by one pixel, and
-// the depth test is taken against the max depth over that bbox with a 1 mm slack.
-__device__ inline bool cull_brick(const Vol& v, const Frame& fr, int bx, int by, int bz) {
-    int lo[3] = {bx * kBrickEdge, by * kBrickEdge, bz * kBrickEdge};
-    int hi[3];
+// Conservative cull of one brick against one frame.  True = some voxel of the brick MAY pass the
+// reference's masks (grid_fusion.py:273-290); a brick with a valid voxel is never dropped.  The
+// brick's corner voxels are transformed (one corner in f64, the rest by f32 edge vectors) and
+// projected in f32; every tolerance is covered by margins: 1 px on the bbox (projected bbox only
+// when the whole brick is >= 0.2 m in front of the camera, where the f32 error is < 0.4 px),
+// 0.1 mm on z <= 0, and 1 mm on the depth test against the max depth over the bbox.
+struct BrickBox {
+    double p0[3];  // world position of the low corner voxel (f64, exact lattice)
+    float ext[3];  // (hi - lo) * vs per axis
+};
+
+__device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz) {
+    const int bb[3] = {bx, by, bz};
+    BrickBox r;
+#pragma unroll
     for (int a = 0; a < 3; ++a) {
-        hi[a] = min(lo[a] + kBrickEdge - 1, v.dims[a] - 1) + v.off[a];
-        lo[a] += v.off[a];
+        const int lo = bb[a] * kBrickEdge;
+        const int hi = min(lo + kBrickEdge - 1, v.dims[a] - 1);
+        r.p0[a] = (double)v.origin[a] + v.vs * (double)(lo + v.off[a]);
+        r.ext[a] = (float)(v.vs * (double)(hi - lo));
     }
-    double zmin = 1e300, zmax = -1e300, umin = 1e300, umax = -1e300, vmin = 1e300, vmax = -1e300;
+    return r;
+}
+
+__device__ inline bool cull_brick(const Vol& v, const Frame& fr, const BrickBox& bb) {
+    const double* T = fr.T;
+    float c0[3], d[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        c0[r] = (float)(T[4 * r + 0] * bb.p0[0] + T[4 * r + 1] * bb.p0[1] + T[4 * r + 2] * bb.p0[2] + T[4 * r + 3]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) d[r][a] = (float)T[4 * r + a] * bb.ext[a];
+    }
+    const float fx = (float)fr.fx, fy = (float)fr.fy, cx = (float)fr.cx, cy = (float)fr.cy;
+    float zmin = 3e38f, zmax = -3e38f, umin = 3e38f, umax = -3e38f, vmin = 3e38f, vmax = -3e38f;
+#pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const double px = (double)v.origin[0] + v.vs * (double)((c & 1) ? hi[0] : lo[0]);
-        const double py = (double)v.origin[1] + v.vs * (double)((c & 2) ? hi[1] : lo[1]);
-        const double pz = (double)v.origin[2] + v.vs * (double)((c & 4) ? hi[2] : lo[2]);
-        const double x = fr.T[0] * px + fr.T[1] * py + fr.T[2] * pz + fr.T[3];
-        const double y = fr.T[4] * px + fr.T[5] * py + fr.T[6] * pz + fr.T[7];
-        const double z = fr.T[8] * px + fr.T[9] * py + fr.T[10] * pz + fr.T[11];
-        zmin = fmin(zmin, z);
-        zmax = fmax(zmax, z);
-        const double iz = 1.0 / fmax(z, 1e-9);
-        const double u = fr.fx * x * iz + fr.cx, w = fr.fy * y * iz + fr.cy;
-        umin = fmin(umin, u); umax = fmax(umax, u);
-        vmin = fmin(vmin, w); vmax = fmax(vmax, w);
+        float q[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            q[r] = c0[r] + ((c & 1) ? d[r][0] : 0.0f) + ((c & 2) ? d[r][1] : 0.0f) + ((c & 4) ? d[r][2] : 0.0f);
+        zmin = fminf(zmin, q[2]);
+        zmax = fmaxf(zmax, q[2]);
+        const float iz = __builtin_amdgcn_rcpf(fmaxf(q[2], 1e-6f));
+        const float u = fx * q[0] * iz + cx, w = fy * q[1] * iz + cy;
+        umin = fminf(umin, u); umax = fmaxf(umax, u);
+        vmin = fminf(vmin, w); vmax = fmaxf(vmax, w);
     }
-    if (zmax < -1e-4) return false;  // every voxel has z <= 0
+    if (zmax < -1e-4f) return false;  // every voxel has z <= 0
     int u0 = 0, u1 = fr.W - 1, v0 = 0, v1 = fr.H - 1;
-    if (zmin > 0.02) {  // whole brick in front of the camera: projected hull is convex
-        const double fu0 = floor(umin) - 1.0, fu1 = ceil(umax) + 1.0;
-        const double fv0 = floor(vmin) - 1.0, fv1 = ceil(vmax) + 1.0;
-        if (fu1 < 0.0 || fv1 < 0.0 || fu0 > (double)(fr.W - 1) || fv0 > (double)(fr.H - 1))
-            return false;
-        u0 = (int)fmax(fu0, 0.0); u1 = (int)fmin(fu1, (double)(fr.W - 1));
-        v0 = (int)fmax(fv0, 0.0); v1 = (int)fmin(fv1, (double)(fr.H - 1));
+    if (zmin > 0.2f) {  // whole brick well in front of the camera: projected hull is convex
+        const float fu0 = floorf(umin) - 1.0f, fu1 = ceilf(umax) + 1.0f;
+        const float fv0 = floorf(vmin) - 1.0f, fv1 = ceilf(vmax) + 1.0f;
+        if (fu1 < 0.0f || fv1 < 0.0f || fu0 > (float)(fr.W - 1) || fv0 > (float)(fr.H - 1)) return false;
+        u0 = (int)fmaxf(fu0, 0.0f); u1 = (int)fminf(fu1, (float)(fr.W - 1));
+        v0 = (int)fmaxf(fv0, 0.0f); v1 = (int)fminf(fv1, (float)(fr.H - 1));
     }
     // max depth over the bbox from the smallest pyramid level where it spans <= 4x4 texels
     int L = 1;
     while (L < kPyrLevels && (((u1 >> L) - (u0 >> L)) > 3 || ((v1 >> L) - (v0 >> L)) > 3)) ++L;
-    const float need = (float)(zmin - v.trunc) - 1e-3f;
+    const float need = zmin - (float)v.trunc - 1e-3f;
     const float* lvl = fr.pyr + fr.pyr_off[L];
     const int wl = fr.pyr_w[L];
     float dmax = 0.0f;
     for (int ty = v0 >> L; ty <= (v1 >> L); ++ty)
-        for (int tx = u0 >> L; tx <= (u1 >> L); ++tx) {
-            dmax = fmaxf(dmax, lvl[ty * wl + tx]);
-        }
+        for (int tx = u0 >> L; tx <= (u1 >> L); ++tx) dmax = fmaxf(dmax, lvl[ty * wl + tx]);
     return dmax > 0.0f && dmax >= need;
 }
 
@@ -291,17 +319,21 @@ __device__ inline double readlane_f64(double x, int l) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-brick integrate, one wave.  Lane (x,y) = (lane>>3, lane&7) owns the z-column of the brick
-// and walks z = 0..7: the x/y part of the camera transform is computed once per column, and the
-// brick-local layout [x][y][z] makes the column 32 contiguous bytes per field, so the state moves
-// with two 16-byte loads/stores per field per lane (a wave: one contiguous 2 KB segment).  The
-// 8 z-steps go through the phases together (project -> gather depth -> test -> load state and
-// colour -> update -> store) to keep many loads in flight per lane.
+// Per-brick integrate, one wave, over the frames of a batch in which the cull kept the brick.
+// Lane (x,y) = (lane>>3, lane&7) owns the z-column of the brick and walks z = 0..7: the x/y part
+// of the camera transform is computed once per column, and the brick-local layout [x][y][z]
+// makes the column 32 contiguous bytes per field, so the state moves with 16-byte loads/stores
+// (a wave: one contiguous 2 KB segment per field).  The state stays in registers across the
+// batch's frames (loaded at its first use, stored once at the end); within a frame the 8 z-steps
+// go through the phases together (project -> gather depth -> test -> colour -> update) to keep
+// many loads in flight per lane.
 // ---------------------------------------------------------------------------------------------
 template <bool HASH, int CK>
-__device__ inline void integrate_brick(const Vol& v, const Frame& fr, const Pool& pool,
-                                       const Table& tab, int b, unsigned long long* s_stat) {
+__device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
+                                       const Table& tab, unsigned entry, unsigned long long* s_stat) {
     const int lane = lane_id();
+    const int b = (int)(entry & 0xFFFFFFu);
+    const unsigned fmask = entry >> 24;
     const int nb12 = v.nb[1] * v.nb[2];
     const int bx = b / nb12;
     const int rem = b - bx * nb12;
@@ -311,165 +343,202 @@ __device__ inline void integrate_brick(const Vol& v, const Frame& fr, const Pool
     const int ly = by * kBrickEdge + (lane & 7);
     const bool col_in = lx < v.dims[0] && ly < v.dims[1];
     const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge);
-    // vox2world + the x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:170-181, 363-368)
+    // vox2world (grid_fusion.py:170-181); lanes 0..7 compute the brick's 8 z coordinates
     const double px = vox_world(v.origin[0], v.vs, v.off[0] + lx);
     const double py = vox_world(v.origin[1], v.vs, v.off[1] + ly);
-    const double a0 = fma(fr.T[1], py, fr.T[0] * px);
-    const double a1 = fma(fr.T[5], py, fr.T[4] * px);
-    const double a2 = fma(fr.T[9], py, fr.T[8] * px);
-    // the brick's 8 z world coordinates: lanes 0..7 compute them, every lane reads them back
     const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));
 
-    // phase 1: project (grid_fusion.py:262-277)
-    unsigned cand = 0;
-    int pix[kBrickEdge];
-    double zc[kBrickEdge];
+    float ws[kBrickEdge], ts[kBrickEdge], cs[kBrickEdge];
 #pragma unroll
     for (int k = 0; k < kBrickEdge; ++k) {
-        pix[k] = 0;
-        const double pz = readlane_f64(pz_l, k);
-        const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
-        zc[k] = z;
-        if (!(col_in && k < nz && z > 0.0)) continue;
-        const double x = fr.T[3] + fma(fr.T[2], pz, a0);
-        const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-        const double rz = refined_rcp(z);
-        const double u = exact_pixel(x * fr.fx, z, rz, fr.cx);
-        const double w = exact_pixel(y * fr.fy, z, rz, fr.cy);
-        if (!(u >= 0.0 && u < (double)fr.W && w >= 0.0 && w < (double)fr.H)) continue;
-        pix[k] = (int)w * fr.W + (int)u;
-        cand |= 1u << k;
+        ws[k] = 0.0f;
+        ts[k] = 1.0f;
+        cs[k] = 0.0f;
     }
-    // phase 2: gather depth for every candidate at once
-    double dep[kBrickEdge];
+    unsigned loaded = 0;   // 16-B halves of this lane's column held in registers (bit 0: z 0-3)
+    unsigned dirty = 0;    // halves changed by the batch
+    unsigned touched = 0;  // voxels updated by any frame of the batch (entry bits, hash)
+    long long blk = -1;
+    bool is_new = false;
+    int nupd = 0;
+
+    for (int fi = 0; fi < bt.n; ++fi) {
+        if (!((fmask >> fi) & 1u)) continue;
+        const Frame& fr = bt.f[fi];
+        // x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:363-368)
+        const double a0 = fma(fr.T[1], py, fr.T[0] * px);
+        const double a1 = fma(fr.T[5], py, fr.T[4] * px);
+        const double a2 = fma(fr.T[9], py, fr.T[8] * px);
+        // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
+        // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
+        // pixel lies within 1e-9 px of a rounding boundary are redone exactly afterwards.
+        double zc[kBrickEdge], uu[kBrickEdge], vv[kBrickEdge];
+        unsigned inb = 0, slow = 0;
 #pragma unroll
-    for (int k = 0; k < kBrickEdge; ++k) dep[k] = ((cand >> k) & 1u) ? fr.depthm[pix[k]] : 0.0;
-    // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
-    unsigned vmask = 0;
-    double dist[kBrickEdge];
+        for (int k = 0; k < kBrickEdge; ++k) {
+            const double pz = readlane_f64(pz_l, k);
+            const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
+            const double x = fr.T[3] + fma(fr.T[2], pz, a0);
+            const double y = fr.T[7] + fma(fr.T[6], pz, a1);
+            const double rz = refined_rcp(z);
+            const double sx = (x * fr.fx) * rz + fr.cx, sy = (y * fr.fy) * rz + fr.cy;
+            const double ux = rint(sx), uy = rint(sy);
+            const bool ok = fabs(sx - ux) < 0.5 - 1e-9 && fabs(sy - uy) < 0.5 - 1e-9 &&
+                            fabs(sx) < 1e9 && fabs(sy) < 1e9;
+            const bool in = col_in && k < nz && z > 0.0;
+            zc[k] = z;
+            uu[k] = ux;
+            vv[k] = uy;
+            inb |= (unsigned)in << k;
+            slow |= (unsigned)(in && !ok) << k;
+        }
+        if (__ballot(slow != 0)) {
 #pragma unroll
-    for (int k = 0; k < kBrickEdge; ++k) {
-        const double diff = dep[k] - zc[k];
-        dist[k] = 0.0;
-        if (((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc) {
+            for (int k = 0; k < kBrickEdge; ++k) {
+                if (!((slow >> k) & 1u)) continue;
+                const double pz = readlane_f64(pz_l, k);
+                const double x = fr.T[3] + fma(fr.T[2], pz, a0);
+                const double y = fr.T[7] + fma(fr.T[6], pz, a1);
+                uu[k] = rint((x * fr.fx) / zc[k] + fr.cx);  // the reference's own operation order
+                vv[k] = rint((y * fr.fy) / zc[k] + fr.cy);
+            }
+        }
+        unsigned cand = 0;
+        int pix[kBrickEdge];
+#pragma unroll
+        for (int k = 0; k < kBrickEdge; ++k) {
+            const bool c = ((inb >> k) & 1u) && uu[k] >= 0.0 && uu[k] < (double)fr.W &&
+                           vv[k] >= 0.0 && vv[k] < (double)fr.H;
+            cand |= (unsigned)c << k;
+            pix[k] = c ? (int)vv[k] * fr.W + (int)uu[k] : 0;
+        }
+        // phase 2: gather depth for every step at once (non-candidates read pixel 0, discarded)
+        double dep[kBrickEdge];
+#pragma unroll
+        for (int k = 0; k < kBrickEdge; ++k) dep[k] = fr.depthm[pix[k]];
+        // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
+        unsigned vmask = 0;
+        double dist[kBrickEdge];
+#pragma unroll
+        for (int k = 0; k < kBrickEdge; ++k) {
+            const double diff = dep[k] - zc[k];
+            const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
             const double dd = diff / v.trunc;
             dist[k] = dd > 1.0 ? 1.0 : dd;  // np.minimum(1, .)
-            vmask |= 1u << k;
+            vmask |= (unsigned)ok << k;
         }
-    }
-    if (__ballot(vmask != 0) == 0) return;
+        if (__ballot(vmask != 0) == 0) continue;
 
-    long long blk = b;
-    bool is_new = false;
-    if (HASH) {
-        long long slot = 0, probe = 0;
-        const unsigned long long key = pack_key(bx, by, bz);
-        const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
-        const int r = table_find_or_insert(tab, key, home, true, is_new, slot, probe);
-        if (r < 0) {  // no space: skip the whole brick; the host grows the table and re-runs it
-            if (lane == 0) {
-                const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
-                if ((long long)o < tab.overflow_cap) tab.overflow[o] = b;
-                atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
+        if (blk < 0) {  // first frame of the batch that updates this brick: find its storage
+            if (HASH) {
+                long long slot = 0, probe = 0;
+                const unsigned long long key = pack_key(bx, by, bz);
+                const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
+                const int r = table_find_or_insert(tab, key, home, true, is_new, slot, probe);
+                if (r < 0) {  // no space: skip the brick for the whole batch (nothing written yet);
+                    if (lane == 0) {  // the host grows the table and re-runs it
+                        const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
+                        if ((long long)o < tab.overflow_cap) tab.overflow[o] = (int)entry;
+                        atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
+                    }
+                    return;
+                }
+                blk = r;
+                if (is_new) loaded = 3u;  // a fresh block starts at (1, 0, 0): nothing to load
+                if (lane == 0) {
+                    atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
+                    atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
+                    atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
+                    if (is_new) atomicAdd(&s_stat[ST_ALLOC], 1ull);
+                }
+            } else {
+                blk = b;
             }
-            return;
         }
-        blk = r;
-        if (lane == 0) {
-            atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
-            atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
-            atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
-            if (is_new) atomicAdd(&s_stat[ST_ALLOC], 1ull);
-        }
-    }
-
-    // phase 4: state (two 16-B halves per field, only halves with a valid voxel) and colour
-    const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge;
-    const bool h0 = (vmask & 0x0Fu) != 0, h1 = (vmask & 0xF0u) != 0;
-    float w_old[kBrickEdge], t_old[kBrickEdge], c_old[kBrickEdge];
-#pragma unroll
-    for (int k = 0; k < kBrickEdge; ++k) {
-        w_old[k] = 0.0f;
-        t_old[k] = 1.0f;
-        c_old[k] = 0.0f;
-    }
-    if (!(HASH && is_new)) {
-        if (h0) {
+        const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge;
+        // phase 4: state halves not yet in registers, and the colour of every valid voxel
+        const unsigned need = ((vmask & 0x0Fu) ? 1u : 0u) | ((vmask & 0xF0u) ? 2u : 0u);
+        const unsigned ld = need & ~loaded;
+        if (ld & 1u) {
             const float4 W = *(const float4*)(pool.weight + base);
             const float4 T = *(const float4*)(pool.tsdf + base);
             const float4 C = *(const float4*)(pool.color + base);
-            w_old[0] = W.x; w_old[1] = W.y; w_old[2] = W.z; w_old[3] = W.w;
-            t_old[0] = T.x; t_old[1] = T.y; t_old[2] = T.z; t_old[3] = T.w;
-            c_old[0] = C.x; c_old[1] = C.y; c_old[2] = C.z; c_old[3] = C.w;
+            ws[0] = W.x; ws[1] = W.y; ws[2] = W.z; ws[3] = W.w;
+            ts[0] = T.x; ts[1] = T.y; ts[2] = T.z; ts[3] = T.w;
+            cs[0] = C.x; cs[1] = C.y; cs[2] = C.z; cs[3] = C.w;
         }
-        if (h1) {
+        if (ld & 2u) {
             const float4 W = *(const float4*)(pool.weight + base + 4);
             const float4 T = *(const float4*)(pool.tsdf + base + 4);
             const float4 C = *(const float4*)(pool.color + base + 4);
-            w_old[4] = W.x; w_old[5] = W.y; w_old[6] = W.z; w_old[7] = W.w;
-            t_old[4] = T.x; t_old[5] = T.y; t_old[6] = T.z; t_old[7] = T.w;
-            c_old[4] = C.x; c_old[5] = C.y; c_old[6] = C.z; c_old[7] = C.w;
+            ws[4] = W.x; ws[5] = W.y; ws[6] = W.z; ws[7] = W.w;
+            ts[4] = T.x; ts[5] = T.y; ts[6] = T.z; ts[7] = T.w;
+            cs[4] = C.x; cs[5] = C.y; cs[6] = C.z; cs[7] = C.w;
+        }
+        loaded |= need;
+        dirty |= need;
+        touched |= vmask;
+        unsigned cpx[kBrickEdge];
+#pragma unroll
+        for (int k = 0; k < kBrickEdge; ++k) {
+            const int p = ((vmask >> k) & 1u) ? pix[k] : 0;
+            cpx[k] = (CK == 0) ? fr.rgbx[p] : __float_as_uint(((const float*)fr.color)[p]);
+        }
+        // phase 5: update in registers, straight-line; invalid steps keep their old values
+#pragma unroll
+        for (int k = 0; k < kBrickEdge; ++k) {
+            const bool ok = (vmask >> k) & 1u;
+            const float w_old = ws[k];
+            // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average
+            const float wn = (float)((double)w_old + fr.ow);
+            const float wt = w_old * ts[k];
+            const float tn = (float)(((double)wt + fr.ow * dist[k]) / (double)wn);
+            // colour (grid_fusion.py:302-314): float32 throughout, round half to even
+            float nb, ng, nr;
+            if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
+                nr = (float)(cpx[k] & 0xFFu);
+                ng = (float)((cpx[k] >> 8) & 0xFFu);
+                nb = (float)((cpx[k] >> 16) & 0xFFu);
+            } else {
+                const float nc = __uint_as_float(cpx[k]);
+                nb = floorf(nc / 65536.0f);
+                ng = floorf((nc - nb * 65536.0f) / 256.0f);
+                nr = nc - nb * 65536.0f - ng * 256.0f;
+            }
+            const float co = cs[k];
+            const float ob = floorf(co / 65536.0f);
+            const float og = floorf((co - ob * 65536.0f) / 256.0f);
+            const float orr = co - ob * 65536.0f - og * 256.0f;
+            const float cb = fminf(255.0f, rintf((w_old * ob + fr.ow32 * nb) / wn));
+            const float cg = fminf(255.0f, rintf((w_old * og + fr.ow32 * ng) / wn));
+            const float cr = fminf(255.0f, rintf((w_old * orr + fr.ow32 * nr) / wn));
+            const float cn = cb * 65536.0f + cg * 256.0f + cr;
+            ws[k] = ok ? wn : ws[k];
+            ts[k] = ok ? tn : ts[k];
+            cs[k] = ok ? cn : cs[k];
+            nupd += ok ? 1 : 0;
         }
     }
-    unsigned cpx[kBrickEdge];
-#pragma unroll
-    for (int k = 0; k < kBrickEdge; ++k) {
-        cpx[k] = 0u;
-        if ((vmask >> k) & 1u) cpx[k] = (CK == 0) ? fr.rgbx[pix[k]] : __float_as_uint(((const float*)fr.color)[pix[k]]);
+    if (blk < 0) return;  // no frame of the batch updated this brick
+
+    // phase 6: store the changed halves once (a new hash block is written whole: its init)
+    const unsigned st = dirty | ((HASH && is_new) ? 3u : 0u);
+    const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge;
+    if (st & 1u) {
+        *(float4*)(pool.weight + base) = make_float4(ws[0], ws[1], ws[2], ws[3]);
+        *(float4*)(pool.tsdf + base) = make_float4(ts[0], ts[1], ts[2], ts[3]);
+        *(float4*)(pool.color + base) = make_float4(cs[0], cs[1], cs[2], cs[3]);
     }
-    // phase 5: update
-    int nupd = 0;
-    float w_new[kBrickEdge], t_new[kBrickEdge], c_new[kBrickEdge];
-#pragma unroll
-    for (int k = 0; k < kBrickEdge; ++k) {
-        w_new[k] = w_old[k];
-        t_new[k] = t_old[k];
-        c_new[k] = c_old[k];
-        if (!((vmask >> k) & 1u)) continue;
-        // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average
-        const float wn = (float)((double)w_old[k] + fr.ow);
-        const float wt = w_old[k] * t_old[k];
-        t_new[k] = (float)(((double)wt + fr.ow * dist[k]) / (double)wn);
-        w_new[k] = wn;
-        // colour (grid_fusion.py:302-314): float32 throughout, round half to even
-        float nb, ng, nr;
-        if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
-            nr = (float)(cpx[k] & 0xFFu);
-            ng = (float)((cpx[k] >> 8) & 0xFFu);
-            nb = (float)((cpx[k] >> 16) & 0xFFu);
-        } else {
-            const float nc = __uint_as_float(cpx[k]);
-            nb = floorf(nc / 65536.0f);
-            ng = floorf((nc - nb * 65536.0f) / 256.0f);
-            nr = nc - nb * 65536.0f - ng * 256.0f;
-        }
-        const float co = c_old[k];
-        const float ob = floorf(co / 65536.0f);
-        const float og = floorf((co - ob * 65536.0f) / 256.0f);
-        const float orr = co - ob * 65536.0f - og * 256.0f;
-        const float cb = fminf(255.0f, rintf((w_old[k] * ob + fr.ow32 * nb) / wn));
-        const float cg = fminf(255.0f, rintf((w_old[k] * og + fr.ow32 * ng) / wn));
-        const float cr = fminf(255.0f, rintf((w_old[k] * orr + fr.ow32 * nr) / wn));
-        c_new[k] = cb * 65536.0f + cg * 256.0f + cr;
-        ++nupd;
-    }
-    // phase 6: store the halves that changed (a new hash block is written whole: its init)
-    const bool s0 = h0 || (HASH && is_new), s1 = h1 || (HASH && is_new);
-    if (s0) {
-        *(float4*)(pool.weight + base) = make_float4(w_new[0], w_new[1], w_new[2], w_new[3]);
-        *(float4*)(pool.tsdf + base) = make_float4(t_new[0], t_new[1], t_new[2], t_new[3]);
-        *(float4*)(pool.color + base) = make_float4(c_new[0], c_new[1], c_new[2], c_new[3]);
-    }
-    if (s1) {
-        *(float4*)(pool.weight + base + 4) = make_float4(w_new[4], w_new[5], w_new[6], w_new[7]);
-        *(float4*)(pool.tsdf + base + 4) = make_float4(t_new[4], t_new[5], t_new[6], t_new[7]);
-        *(float4*)(pool.color + base + 4) = make_float4(c_new[4], c_new[5], c_new[6], c_new[7]);
+    if (st & 2u) {
+        *(float4*)(pool.weight + base + 4) = make_float4(ws[4], ws[5], ws[6], ws[7]);
+        *(float4*)(pool.tsdf + base + 4) = make_float4(ts[4], ts[5], ts[6], ts[7]);
+        *(float4*)(pool.color + base + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
     }
     if (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns the block this launch
         unsigned long long mine = 0;
 #pragma unroll
         for (int k = 0; k < kBrickEdge; ++k) {
-            const unsigned long long m = __ballot((vmask >> k) & 1u);
+            const unsigned long long m = __ballot((touched >> k) & 1u);
             if (lane == k) mine = m;
         }
         if (lane < kBrickEdge) {
@@ -495,10 +564,11 @@ __device__ inline void flush_stats(unsigned long long* s_stat, unsigned long lon
     }
 }
 
-// Conservative cull of every brick (one lane each) and compaction of the survivors into a
-// frame-wide list: wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
+// Conservative cull of every brick (one lane each) against every frame of the batch, and
+// compaction of the bricks seen by at least one frame into a list of (brick | frame mask << 24):
+// wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
 template <bool HASH>
-__global__ __launch_bounds__(kWG) void k_cull(Vol v, Frame fr, Table tab, int* list,
+__global__ __launch_bounds__(kWG) void k_cull(Vol v, Batch bt, Table tab, unsigned* list,
                                              unsigned int* count, unsigned long long* stats) {
     __shared__ int s_cnt[kWG / 64];
     __shared__ unsigned int s_base;
@@ -507,18 +577,23 @@ __global__ __launch_bounds__(kWG) void k_cull(Vol v, Frame fr, Table tab, int* l
     if (tid < kNStat) s_stat[tid] = 0;
     const long long nbricks = (long long)v.nb[0] * v.nb[1] * v.nb[2];
     const long long e = (long long)blockIdx.x * kWG + tid;
-    bool keep = false;
+    unsigned fmask = 0;
     if (e < nbricks) {
         const int b = (int)e;
         const int nb12 = v.nb[1] * v.nb[2];
         const int bx = b / nb12, rem = b - bx * nb12, by = rem / v.nb[2], bz = rem - by * v.nb[2];
-        keep = true;
+        bool mine = true;
         if (HASH && v.n_shards > 1) {  // bucket-range ownership
             const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
-            keep = (int)((home * v.n_shards) / tab.capacity) == v.shard;
+            mine = (int)((home * v.n_shards) / tab.capacity) == v.shard;
         }
-        if (keep) keep = cull_brick(v, fr, bx, by, bz);
+        if (mine) {
+            const BrickBox box = brick_box(v, bx, by, bz);
+            for (int f = 0; f < bt.n; ++f)
+                if (cull_brick(v, bt.f[f], box)) fmask |= 1u << f;
+        }
     }
+    const bool keep = fmask != 0;
     const unsigned long long m = __ballot(keep);
     if (lane == 0) s_cnt[wave] = __popcll(m);
     __syncthreads();
@@ -532,17 +607,17 @@ __global__ __launch_bounds__(kWG) void k_cull(Vol v, Frame fr, Table tab, int* l
     int off = 0;
 #pragma unroll
     for (int w = 0; w < kWG / 64; ++w) off += (w < wave) ? s_cnt[w] : 0;
-    if (keep) list[s_base + off + __popcll(m & ((1ull << lane) - 1ull))] = (int)e;
+    if (keep) list[s_base + off + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)e | (fmask << 24);
     flush_stats(s_stat, stats);
 }
 
 // Integrate the listed bricks: each wave takes list entries gw, gw + NW, ... (NW = waves in the
-// grid), so the work is spread evenly whatever the frame sees.  `count` (device) gives the list
-// length written by k_cull; with count == nullptr the first n_list entries are used (hash
-// overflow re-run).
+// grid, all resident), so the work is spread evenly whatever the frames see.  `count` (device)
+// gives the list length written by k_cull; with count == nullptr the first n_list entries are
+// used (hash overflow re-run).
 template <bool HASH, int CK>
-__global__ __launch_bounds__(kWG) void k_integrate(Vol v, Frame fr, Pool pool, Table tab,
-                                                  unsigned long long* stats, const int* list,
+__global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
+                                                  unsigned long long* stats, const unsigned* list,
                                                   unsigned int* count, int n_list) {
     __shared__ unsigned long long s_stat[kNStat];
     const int tid = threadIdx.x;
@@ -551,7 +626,7 @@ __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Frame fr, Pool pool, T
     const int n = count ? (int)coh_load(count) : n_list;
     const int nw = gridDim.x * (kWG / 64);
     for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
-        integrate_brick<HASH, CK>(v, fr, pool, tab, list[e], s_stat);
+        integrate_brick<HASH, CK>(v, bt, pool, tab, list[e], s_stat);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
@@ -575,12 +650,15 @@ __device__ inline void pyr_level(const Frame& fr, float* pyr, int L, const float
 }
 
 template <int DK, int CK>
-__global__ __launch_bounds__(1024) void k_prep(Frame fr, float* pyr, double* depthm, unsigned* rgbx,
-                                              unsigned int* count) {
+__global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
     __shared__ float sa[32][33];
     __shared__ float sb[32][33];
+    const Frame& fr = bt.f[blockIdx.z];
+    float* pyr = (float*)fr.pyr;
+    double* depthm = (double*)fr.depthm;
+    unsigned* rgbx = (unsigned*)fr.rgbx;
     const int t = threadIdx.x, r = t >> 5, c = t & 31;
-    if (count && t == 0 && blockIdx.x == 0 && blockIdx.y == 0) coh_store(count, 0u);
+    if (count && t == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count, 0u);
     const int x0 = blockIdx.x * 64 + c * 2, y0 = blockIdx.y * 64 + r * 2;
     float m1 = 0.0f;
 #pragma unroll

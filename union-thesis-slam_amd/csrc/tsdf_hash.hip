@@ -20,7 +20,7 @@ struct tsdf_hash {
     Base b;
     Table t{};          // device view (pointers + capacity)
     PoolState host_st{};
-    int* d_list = nullptr;  // re-run list
+    unsigned* d_list = nullptr;  // re-run list
     int list_cap = 0;
 };
 
@@ -355,17 +355,18 @@ int ensure_room(tsdf_hash* h) {
     return TSDF_OK;
 }
 
-// One hash integrate pass: the listed bricks (list/count from k_cull, or an explicit list).
-void launch_integrate(tsdf_hash* h, const Frame& fr, int ck, const int* list, unsigned int* count,
+// One hash integrate pass over a batch: the listed bricks (list/count from k_cull, or an
+// explicit list of skipped entries).
+void launch_integrate(tsdf_hash* h, const Batch& bt, int ck, const unsigned* list, unsigned int* count,
                       int n_list) {
     Base& B = h->b;
     const void* kern = ck == TSDF_COLOR_RGB8 ? (const void*)k_integrate<true, 0> : (const void*)k_integrate<true, 1>;
     const unsigned grid = B.grid_for(kern);
     if (ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_integrate<true, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t,
+        hipLaunchKernelGGL((k_integrate<true, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
                            B.stats, list, count, n_list);
     else
-        hipLaunchKernelGGL((k_integrate<true, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, fr, B.pool, h->t,
+        hipLaunchKernelGGL((k_integrate<true, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
                            B.stats, list, count, n_list);
 }
 
@@ -374,26 +375,27 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
     const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
-    const bool sync_each = !(flags & TSDF_ASYNC) && n_frames == 1;
-    for (int f = 0; f < n_frames; ++f) {
-        Frame fr;
+    const bool sync = !(flags & TSDF_ASYNC);
+    for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
+        Batch bt;
+        const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
-        TSDF_TRY(B.prepare_frame(&fr, depth, dk, color, ck, H, W, K, Tinv + 16 * (size_t)f, 1.0, flags, f));
-        TSDF_TRY(B.launch_prep(fr, dk, ck));
-        hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, fr, h->t, B.list,
+        TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, nullptr, 1.0, flags, f0, n));
+        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H));
+        hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, bt, h->t, B.list,
                            B.count, B.stats);
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
-        launch_integrate(h, fr, ck, (const int*)B.list, B.count, 0);
+        launch_integrate(h, bt, ck, (const unsigned*)B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
         TSDF_HIP(hipGetLastError());
-        ++B.frames;
-        if (!sync_each) continue;
-        // Synchronous frame: recover from a full table/pool exactly (the skipped bricks were
-        // not touched), then keep the reference's load-factor policy for the next frame.
+        B.frames += n;
+        if (!sync) continue;
+        // Synchronous: recover from a full table/pool exactly (the skipped bricks were not
+        // touched by any frame of the batch), then keep the reference's load-factor policy.
         TSDF_TRY(read_state(h));
         for (int round = 0; h->host_st.n_overflow > 0 && round < 40; ++round) {
             const long long n_ov = h->host_st.n_overflow;
@@ -401,19 +403,16 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
                 return set_error(TSDF_E_CAPACITY, "overflow list exceeded (%lld bricks)", n_ov);
             if (h->list_cap < n_ov) {
                 if (h->d_list) (void)hipFree(h->d_list);
-                TSDF_HIP(hipMalloc(&h->d_list, sizeof(int) * n_ov));
+                TSDF_HIP(hipMalloc(&h->d_list, sizeof(unsigned) * n_ov));
                 h->list_cap = (int)n_ov;
             }
-            TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(int) * n_ov, hipMemcpyDeviceToDevice, B.stream));
+            TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(unsigned) * n_ov, hipMemcpyDeviceToDevice, B.stream));
             TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
-            // grow: double the pool if it is the limit, else the table
-            InfoDev inf{};
-            TSDF_TRY(info_raw(h, &inf));
             if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
                 TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
             else
                 TSDF_TRY(resize_table(h, h->t.capacity * 2));
-            launch_integrate(h, fr, ck, h->d_list, nullptr, (int)n_ov);
+            launch_integrate(h, bt, ck, h->d_list, nullptr, (int)n_ov);
             TSDF_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
             TSDF_HIP(hipGetLastError());
@@ -422,14 +421,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         if (h->host_st.n_overflow > 0) return set_error(TSDF_E_CAPACITY, "could not make room in the hash table");
         TSDF_TRY(ensure_room(h));
     }
-    if (!(flags & TSDF_ASYNC) && !sync_each) {
-        TSDF_TRY(read_state(h));
-        if (h->host_st.n_overflow > 0)
-            return set_error(TSDF_E_CAPACITY,
-                             "batch ran out of table/pool space (%lld bricks skipped); create the table "
-                             "with more capacity/max_blocks or integrate frame by frame",
-                             (long long)h->host_st.n_overflow);
-    }
+    if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;
 }
 

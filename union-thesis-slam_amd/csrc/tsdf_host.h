@@ -58,11 +58,11 @@ struct Base {
     Vol vol{};
     Pool pool{};
     long long n_bricks = 0;
-    float* pyr = nullptr;
-    double* depthm = nullptr;  // per-frame f64 metres image (u16 input)
-    unsigned* rgbx = nullptr;  // per-frame packed RGB8 image
+    float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
+    double* depthm = nullptr;  // kMaxBatch per-frame f64 metres images (u16 input)
+    unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
     int pyr_H = 0, pyr_W = 0;
-    int* list = nullptr;        // per-frame list of bricks that survive the cull
+    unsigned* list = nullptr;   // per-batch list of (brick | frame mask << 24) kept by the cull
     unsigned int* count = nullptr;
     int n_cu = 256;             // compute units of the device
     PyrLayout lay{};
@@ -78,11 +78,12 @@ struct Base {
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
     int ensure_pyr(int H, int W);
-    // Builds the frame constants, staging host inputs to the device when needed.
-    int prepare_frame(Frame* fr, const void* depth, int dk, const void* color, int ck, int H,
-                      int W, const double K[9], const double Tinv[16], double ow, int flags,
-                      int frame_index);
-    int launch_prep(const Frame& fr, int dk, int ck);
+    // Frame constants of frames [first, first+n) (n <= kMaxBatch) of a call, each with its own
+    // per-frame buffers; host inputs are staged to the device when needed.
+    int prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
+                      int W, const double K[9], const double* Tinv, const double* ow,
+                      double ow_default, int flags, int first, int n);
+    int launch_prep(const Batch& bt, int dk, int ck, int W, int H);
     // Workgroups of the integrate kernel: as many as can be resident (occupancy x CUs), capped
     // by the work there can be (4 bricks per workgroup per round).
     unsigned grid_for(const void* kernel);
