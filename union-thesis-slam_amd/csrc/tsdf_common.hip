@@ -154,6 +154,28 @@ int check_frame_args(const void* depth, int dk, const void* color, int ck, int H
     return TSDF_OK;
 }
 
+// World-space half-spaces n.p + d >= 0 (unit n) that contain every voxel the reference can
+// update for this frame: z > 0 and -0.5 <= u < W - 0.5, -0.5 <= v < H - 0.5, each widened by
+// one pixel (grid_fusion.py:273-277).  Camera-space plane (a, b, c, e) maps to world space
+// through the rows of world_to_cam.
+static void frustum_planes(Frame* fr, const double* T, int W, int H) {
+    const double cam[5][4] = {{0.0, 0.0, 1.0, 1e-4},
+                              {fr->fx, 0.0, fr->cx + 1.5, 0.0},
+                              {-fr->fx, 0.0, (double)W + 0.5 - fr->cx, 0.0},
+                              {0.0, fr->fy, fr->cy + 1.5, 0.0},
+                              {0.0, -fr->fy, (double)H + 0.5 - fr->cy, 0.0}};
+    for (int i = 0; i < 5; ++i) {
+        double n[3], d = cam[i][3];
+        for (int a = 0; a < 3; ++a)
+            n[a] = cam[i][0] * T[0 + a] + cam[i][1] * T[4 + a] + cam[i][2] * T[8 + a];
+        d += cam[i][0] * T[3] + cam[i][1] * T[7] + cam[i][2] * T[11];
+        const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        const double s = len > 0.0 ? 1.0 / len : 0.0;
+        for (int a = 0; a < 3; ++a) fr->planes[i][a] = (float)(n[a] * s);
+        fr->planes[i][3] = (float)(d * s) + (len > 0.0 ? 1e-4f : 1.0f);  // slack for f32 rounding
+    }
+}
+
 int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
                         int W, const double K[9], const double* Tinv, const double* ow,
                         double ow_default, int flags, int first, int n) {
@@ -199,6 +221,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->color = c + cbytes * i;
         fr->rgbx = rgbx + npx * i;
         fr->pyr = pyr + (size_t)lay.total * i;
+        frustum_planes(fr, T, W, H);
         for (int L = 0; L <= kPyrLevels; ++L) {
             fr->pyr_off[L] = lay.off[L];
             fr->pyr_w[L] = lay.w[L];

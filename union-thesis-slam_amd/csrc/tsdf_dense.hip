@@ -45,8 +45,7 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     TSDF_HIP(hipSetDevice(B.device));
     const Table no_table{};
     const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
-    const unsigned grid0 = B.grid_for((const void*)k_integrate<false, 0>);
-    const unsigned grid1 = B.grid_for((const void*)k_integrate<false, 1>);
+    const unsigned grid = B.grid_for((const void*)k_integrate<false, 0, false>);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
@@ -57,12 +56,21 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
-        if (ck == TSDF_COLOR_RGB8)
-            hipLaunchKernelGGL((k_integrate<false, 0>), dim3(grid0), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
-                               no_table, B.stats, (const unsigned*)B.list, B.count, 0);
+        bool ow1 = true;
+        for (int i = 0; i < n; ++i) ow1 = ow1 && bt.f[i].ow == 1.0;
+        const unsigned* L = (const unsigned*)B.list;
+        if (ck == TSDF_COLOR_RGB8 && ow1)
+            hipLaunchKernelGGL((k_integrate<false, 0, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
+                               no_table, B.stats, L, B.count, 0);
+        else if (ck == TSDF_COLOR_RGB8)
+            hipLaunchKernelGGL((k_integrate<false, 0, false>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
+                               no_table, B.stats, L, B.count, 0);
+        else if (ow1)
+            hipLaunchKernelGGL((k_integrate<false, 1, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
+                               no_table, B.stats, L, B.count, 0);
         else
-            hipLaunchKernelGGL((k_integrate<false, 1>), dim3(grid1), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
-                               no_table, B.stats, (const unsigned*)B.list, B.count, 0);
+            hipLaunchKernelGGL((k_integrate<false, 1, false>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
+                               no_table, B.stats, L, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         B.frames += n;

@@ -50,6 +50,7 @@ struct Frame {
     const void* color;        // the caller's colour (RGB8 or folded f32)
     const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
+    float planes[5][4];       // world-space half-spaces containing every valid voxel (cull)
     int pyr_off[kPyrLevels + 1];
     int pyr_w[kPyrLevels + 1];
     int pyr_h[kPyrLevels + 1];
@@ -144,6 +145,8 @@ __device__ inline double vox_world(float origin, double vs, int g) {
 struct BrickBox {
     double p0[3];  // world position of the low corner voxel (f64, exact lattice)
     float ext[3];  // (hi - lo) * vs per axis
+    float ctr[3];  // centre of the voxel-centre box
+    float rad;     // its half diagonal + 0.1 mm
 };
 
 __device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz) {
@@ -155,11 +158,20 @@ __device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz) {
         const int hi = min(lo + kBrickEdge - 1, v.dims[a] - 1);
         r.p0[a] = (double)v.origin[a] + v.vs * (double)(lo + v.off[a]);
         r.ext[a] = (float)(v.vs * (double)(hi - lo));
+        r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(hi - lo));
     }
+    r.rad = 0.5f * sqrtf(r.ext[0] * r.ext[0] + r.ext[1] * r.ext[1] + r.ext[2] * r.ext[2]) + 1e-4f;
     return r;
 }
 
 __device__ inline bool cull_brick(const Vol& v, const Frame& fr, const BrickBox& bb) {
+    // early out: the brick's bounding sphere entirely outside one of the frustum half-spaces
+    // (z > 0 and -0.5 <= u < W - 0.5, -0.5 <= v < H - 0.5, each widened by 1 px)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const float* q = fr.planes[i];
+        if (q[0] * bb.ctr[0] + q[1] * bb.ctr[1] + q[2] * bb.ctr[2] + q[3] < -bb.rad) return false;
+    }
     const double* T = fr.T;
     float c0[3], d[3][3];
 #pragma unroll
@@ -290,25 +302,15 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 
 
 // ---------------------------------------------------------------------------------------------
-// Pixel of a camera-space coordinate, exactly as cam2pix (grid_fusion.py:195-196):
-// rint(RN(RN(a / z) + c)) with a = RN(x * f).  Fast path: a reciprocal of z refined to ~1 ulp
-// gives s within ~1e-12 px of the exact sum (|s| < ~1e3, the only range where the pixel can be
-// valid); unless s is within 1e-9 px of a rounding boundary rint(s) is then the exact pixel.
-// Otherwise recompute with the reference's own operation order.
+// Reciprocal of z for the fast pixel path.  v_rcp_f64 is accurate to 2^-24.4 and one Newton step
+// brings it to 2^-48.7 (measured over z in [1e-3, 1e3]: tools/gpu/rcp_probe.hip),
+// so u = (x*fx)*rz + cx lies within ~1e-11 px of the reference's (x*fx)/z + cx wherever a pixel
+// can be valid (|u| < 1e3).  Steps whose u is within 1e-9 px of a rounding boundary (or not
+// finite) are recomputed with the reference's own division.
 // ---------------------------------------------------------------------------------------------
-__device__ inline double exact_pixel(double a, double z, double rz, double c) {
-    const double s = a * rz + c;  // -ffp-contract=off: two roundings
-    const double r = rint(s);
-    if (fabs(s - r) < 0.5 - 1e-9 && fabs(s) < 1e9) return r;
-    return rint(a / z + c);
-}
-
 __device__ inline double refined_rcp(double z) {
-    double y = __builtin_amdgcn_rcp(z);
-    double e = fma(-z, y, 1.0);
-    y = fma(y, e, y);
-    e = fma(-z, y, 1.0);
-    return fma(y, e, y);
+    const double y = __builtin_amdgcn_rcp(z);
+    return fma(y, fma(-z, y, 1.0), y);
 }
 
 __device__ inline double readlane_f64(double x, int l) {
@@ -328,7 +330,7 @@ __device__ inline double readlane_f64(double x, int l) {
 // go through the phases together (project -> gather depth -> test -> colour -> update) to keep
 // many loads in flight per lane.
 // ---------------------------------------------------------------------------------------------
-template <bool HASH, int CK>
+template <bool HASH, int CK, bool OW1>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, unsigned entry, unsigned long long* s_stat) {
     const int lane = lane_id();
@@ -383,8 +385,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const double rz = refined_rcp(z);
             const double sx = (x * fr.fx) * rz + fr.cx, sy = (y * fr.fy) * rz + fr.cy;
             const double ux = rint(sx), uy = rint(sy);
-            const bool ok = fabs(sx - ux) < 0.5 - 1e-9 && fabs(sy - uy) < 0.5 - 1e-9 &&
-                            fabs(sx) < 1e9 && fabs(sy) < 1e9;
+            // (a NaN fails both tests; far-out |s| may round differently but is invalid either way)
+            const bool ok = fabs(sx - ux) < 0.5 - 1e-9 && fabs(sy - uy) < 0.5 - 1e-9;
             const bool in = col_in && k < nz && z > 0.0;
             zc[k] = z;
             uu[k] = ux;
@@ -490,9 +492,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const bool ok = (vmask >> k) & 1u;
             const float w_old = ws[k];
             // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average
-            const float wn = (float)((double)w_old + fr.ow);
+            // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
+            const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
             const float wt = w_old * ts[k];
-            const float tn = (float)(((double)wt + fr.ow * dist[k]) / (double)wn);
+            const float tn = (float)(((double)wt + (OW1 ? dist[k] : fr.ow * dist[k])) / (double)wn);
             // colour (grid_fusion.py:302-314): float32 throughout, round half to even
             float nb, ng, nr;
             if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
@@ -509,9 +512,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float ob = floorf(co / 65536.0f);
             const float og = floorf((co - ob * 65536.0f) / 256.0f);
             const float orr = co - ob * 65536.0f - og * 256.0f;
-            const float cb = fminf(255.0f, rintf((w_old * ob + fr.ow32 * nb) / wn));
-            const float cg = fminf(255.0f, rintf((w_old * og + fr.ow32 * ng) / wn));
-            const float cr = fminf(255.0f, rintf((w_old * orr + fr.ow32 * nr) / wn));
+            const float cb = fminf(255.0f, rintf((w_old * ob + (OW1 ? nb : fr.ow32 * nb)) / wn));
+            const float cg = fminf(255.0f, rintf((w_old * og + (OW1 ? ng : fr.ow32 * ng)) / wn));
+            const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
             const float cn = cb * 65536.0f + cg * 256.0f + cr;
             ws[k] = ok ? wn : ws[k];
             ts[k] = ok ? tn : ts[k];
@@ -615,7 +618,7 @@ __global__ __launch_bounds__(kWG) void k_cull(Vol v, Batch bt, Table tab, unsign
 // grid, all resident), so the work is spread evenly whatever the frames see.  `count` (device)
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
-template <bool HASH, int CK>
+template <bool HASH, int CK, bool OW1>
 __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
                                                   unsigned long long* stats, const unsigned* list,
                                                   unsigned int* count, int n_list) {
@@ -626,7 +629,7 @@ __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, T
     const int n = count ? (int)coh_load(count) : n_list;
     const int nw = gridDim.x * (kWG / 64);
     for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
-        integrate_brick<HASH, CK>(v, bt, pool, tab, list[e], s_stat);
+        integrate_brick<HASH, CK, OW1>(v, bt, pool, tab, list[e], s_stat);
     __syncthreads();
     flush_stats(s_stat, stats);
 }

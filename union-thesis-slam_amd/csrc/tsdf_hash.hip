@@ -360,13 +360,13 @@ int ensure_room(tsdf_hash* h) {
 void launch_integrate(tsdf_hash* h, const Batch& bt, int ck, const unsigned* list, unsigned int* count,
                       int n_list) {
     Base& B = h->b;
-    const void* kern = ck == TSDF_COLOR_RGB8 ? (const void*)k_integrate<true, 0> : (const void*)k_integrate<true, 1>;
+    const void* kern = ck == TSDF_COLOR_RGB8 ? (const void*)k_integrate<true, 0, true> : (const void*)k_integrate<true, 1, true>;
     const unsigned grid = B.grid_for(kern);
     if (ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_integrate<true, 0>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
+        hipLaunchKernelGGL((k_integrate<true, 0, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
                            B.stats, list, count, n_list);
     else
-        hipLaunchKernelGGL((k_integrate<true, 1>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
+        hipLaunchKernelGGL((k_integrate<true, 1, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
                            B.stats, list, count, n_list);
 }
 
