@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Turn gpurun_out/profile/ (tools/gpu/run_profile.sh) into the committed profile summaries:
+  profiles/<tag>_kernel_stats.csv      rocprofv3 --kernel-trace --stats of the default bench
+  profiles/<tag>_bench.json            the bench line printed under that profiler
+  profiles/pmc_integrate_<tag>.json    HBM traffic per integrate launch from FETCH_SIZE/WRITE_SIZE
+
+FETCH_SIZE/WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
+coalesced read (MI355X_MICROARCH.md, HBM section); the integrate kernel's HBM reads are its
+16-B/lane brick-state loads (the per-frame depth/colour gathers are L2/MALL-resident), so the
+read side is doubled.  WRITE_SIZE is exact for 16-B/lane stores.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path, counter):
+    out = {}
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] != counter:
+            continue
+        k = row["Kernel_Name"].split("(")[0].replace("void ", "")
+        out.setdefault(k, []).append(float(row["Counter_Value"]))
+    return out
+
+
+def main(tag="r01"):
+    src = os.path.join(REPO, "gpurun_out", "profile")
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    with open(os.path.join(src, "bench_under_rocprof.json")) as f:
+        line = [l for l in f if l.startswith("{")][-1]
+    with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
+        f.write(line)
+    fetch = per_kernel(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
+    summary = {"note": __doc__.strip().splitlines()[-4:], "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        fk = statistics.median(fetch.get(k, [0.0])) * 1024.0
+        wk = statistics.median(write.get(k, [0.0])) * 1024.0
+        summary["kernels"][k] = {"fetch_bytes_raw": fk, "fetch_bytes_corrected": 2 * fk,
+                                 "write_bytes": wk, "hbm_bytes": 2 * fk + wk,
+                                 "launches_sampled": len(fetch.get(k, []))}
+        if k.startswith("tsdf::k_integrate<false"):
+            summary["hbm_bytes_per_launch"] = round(2 * fk + wk)
+            summary["kernel"] = k
+    with open(os.path.join(dst, f"pmc_integrate_{tag}.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

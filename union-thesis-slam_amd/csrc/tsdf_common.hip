@@ -129,15 +129,12 @@ int Base::ensure_pyr(int H, int W) {
     if (pyr) {
         TSDF_HIP(hipStreamSynchronize(stream));
         TSDF_HIP(hipFree(pyr));
-        TSDF_HIP(hipFree(depthm));
         TSDF_HIP(hipFree(rgbx));
         pyr = nullptr;
-        depthm = nullptr;
         rgbx = nullptr;
     }
     lay = pyr_layout(H, W);
     TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total * kMaxBatch));
-    TSDF_HIP(hipMalloc(&depthm, sizeof(double) * (size_t)H * W * kMaxBatch));
     TSDF_HIP(hipMalloc(&rgbx, sizeof(unsigned) * (size_t)H * W * kMaxBatch));
     pyr_H = H;
     pyr_W = W;
@@ -217,7 +214,6 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->H = H;
         fr->W = W;
         fr->depth = d + dbytes * i;
-        fr->depthm = dk == TSDF_DEPTH_U16_MM ? depthm + npx * i : (const double*)(d + dbytes * i);
         fr->color = c + cbytes * i;
         fr->rgbx = rgbx + npx * i;
         fr->pyr = pyr + (size_t)lay.total * i;
@@ -301,7 +297,6 @@ void Base::release() {
     if (stream) (void)hipStreamSynchronize(stream);
     prof.release();
     if (pyr) (void)hipFree(pyr);
-    if (depthm) (void)hipFree(depthm);
     if (rgbx) (void)hipFree(rgbx);
     if (list) (void)hipFree(list);
     if (count) (void)hipFree(count);
@@ -310,7 +305,6 @@ void Base::release() {
     if (st_color) (void)hipFree(st_color);
     if (stream) (void)hipStreamDestroy(stream);
     pyr = nullptr;
-    depthm = nullptr;
     rgbx = nullptr;
     list = nullptr;
     count = nullptr;

@@ -45,7 +45,7 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     TSDF_HIP(hipSetDevice(B.device));
     const Table no_table{};
     const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
-    const unsigned grid = B.grid_for((const void*)k_integrate<false, 0, false>);
+    const unsigned grid = B.grid_for((const void*)k_integrate<false, 0, 0, false>);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
@@ -59,18 +59,23 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
         bool ow1 = true;
         for (int i = 0; i < n; ++i) ow1 = ow1 && bt.f[i].ow == 1.0;
         const unsigned* L = (const unsigned*)B.list;
-        if (ck == TSDF_COLOR_RGB8 && ow1)
-            hipLaunchKernelGGL((k_integrate<false, 0, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
-                               no_table, B.stats, L, B.count, 0);
-        else if (ck == TSDF_COLOR_RGB8)
-            hipLaunchKernelGGL((k_integrate<false, 0, false>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
-                               no_table, B.stats, L, B.count, 0);
-        else if (ow1)
-            hipLaunchKernelGGL((k_integrate<false, 1, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
-                               no_table, B.stats, L, B.count, 0);
-        else
-            hipLaunchKernelGGL((k_integrate<false, 1, false>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool,
-                               no_table, B.stats, L, B.count, 0);
+        const int sel = (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (ck == TSDF_COLOR_RGB8 ? 0 : 2) | (ow1 ? 1 : 0);
+        switch (sel) {
+#define TSDF_LAUNCH(S, DK_, CK_, OW_)                                                                  \
+    case S:                                                                                            \
+        hipLaunchKernelGGL((k_integrate<false, DK_, CK_, OW_>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, \
+                           B.pool, no_table, B.stats, L, B.count, 0);                                  \
+        break;
+            TSDF_LAUNCH(0, 0, 0, false)
+            TSDF_LAUNCH(1, 0, 0, true)
+            TSDF_LAUNCH(2, 0, 1, false)
+            TSDF_LAUNCH(3, 0, 1, true)
+            TSDF_LAUNCH(4, 1, 0, false)
+            TSDF_LAUNCH(5, 1, 0, true)
+            TSDF_LAUNCH(6, 1, 1, false)
+            TSDF_LAUNCH(7, 1, 1, true)
+#undef TSDF_LAUNCH
+        }
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         B.frames += n;

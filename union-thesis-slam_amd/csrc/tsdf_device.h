@@ -45,8 +45,7 @@ struct Frame {
     double ow;                // obs_weight as a Python float (f64)
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
-    const void* depth;        // the caller's depth (u16 mm or f64 m)
-    const double* depthm;     // f64 metres = NumPy's astype(float)/1000. (k_pyramid writes it)
+    const void* depth;        // the caller's depth: u16 millimetres or f64 metres
     const void* color;        // the caller's colour (RGB8 or folded f32)
     const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
@@ -301,6 +300,20 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 }
 
 
+// Depth in metres at pixel p exactly as NumPy computes it: u16 mm -> astype(float) / 1000.
+// (grid_demo1.py:81-82).  For u16 input the quotient is m * 0.001 with one FMA correction
+// (r = m - 1000 q exactly; q + r * 0.001), which equals RN(m / 1000) for every m in [0, 65535]
+// (checked exhaustively: tools/check_depth_conversion.c).
+template <int DK>
+__device__ inline double depth_m(const Frame& fr, int p) {
+    if (DK == 0) {
+        const double m = (double)((const unsigned short*)fr.depth)[p];
+        const double q = m * 0.001;
+        return fma(fma(-q, 1000.0, m), 0.001, q);
+    }
+    return ((const double*)fr.depth)[p];
+}
+
 // ---------------------------------------------------------------------------------------------
 // Reciprocal of z for the fast pixel path.  v_rcp_f64 is accurate to 2^-24.4 and one Newton step
 // brings it to 2^-48.7 (measured over z in [1e-3, 1e3]: tools/gpu/rcp_probe.hip),
@@ -330,7 +343,7 @@ __device__ inline double readlane_f64(double x, int l) {
 // go through the phases together (project -> gather depth -> test -> colour -> update) to keep
 // many loads in flight per lane.
 // ---------------------------------------------------------------------------------------------
-template <bool HASH, int CK, bool OW1>
+template <bool HASH, int DK, int CK, bool OW1>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, unsigned entry, unsigned long long* s_stat) {
     const int lane = lane_id();
@@ -417,7 +430,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // phase 2: gather depth for every step at once (non-candidates read pixel 0, discarded)
         double dep[kBrickEdge];
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) dep[k] = fr.depthm[pix[k]];
+        for (int k = 0; k < kBrickEdge; ++k) dep[k] = depth_m<DK>(fr, pix[k]);
         // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
         unsigned vmask = 0;
         double dist[kBrickEdge];
@@ -618,7 +631,7 @@ __global__ __launch_bounds__(kWG) void k_cull(Vol v, Batch bt, Table tab, unsign
 // grid, all resident), so the work is spread evenly whatever the frames see.  `count` (device)
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
-template <bool HASH, int CK, bool OW1>
+template <bool HASH, int DK, int CK, bool OW1>
 __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
                                                   unsigned long long* stats, const unsigned* list,
                                                   unsigned int* count, int n_list) {
@@ -629,13 +642,13 @@ __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, T
     const int n = count ? (int)coh_load(count) : n_list;
     const int nw = gridDim.x * (kWG / 64);
     for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
-        integrate_brick<HASH, CK, OW1>(v, bt, pool, tab, list[e], s_stat);
+        integrate_brick<HASH, DK, CK, OW1>(v, bt, pool, tab, list[e], s_stat);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
 
-// Per frame, before the cull (one pass over the image): the f64 metres image (u16 input, exactly
-// NumPy's astype(float)/1000.), the packed RGB8 image, the max-depth pyramid levels 1..6
+// Per frame, before the cull (one pass over the image): the packed RGB8 image, the max-depth
+// pyramid levels 1..6
 // (texel = max over a 2^L x 2^L block, metres, 0 for invalid/outside) and the reset of the
 // brick-list counter.  One 1024-thread workgroup per 64x64 tile, 2x2 pixels per thread.
 template <int REDUCE>
@@ -658,7 +671,6 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
     __shared__ float sb[32][33];
     const Frame& fr = bt.f[blockIdx.z];
     float* pyr = (float*)fr.pyr;
-    double* depthm = (double*)fr.depthm;
     unsigned* rgbx = (unsigned*)fr.rgbx;
     const int t = threadIdx.x, r = t >> 5, c = t & 31;
     if (count && t == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count, 0u);
@@ -671,13 +683,8 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
             const int x = x0 + dx, y = y0 + dy;
             if (x < fr.W && y < fr.H) {
                 const int p = y * fr.W + x;
-                double d;
-                if (DK == 0) {  // NumPy: depth.astype(float) / 1000. (grid_demo1.py:81-82)
-                    d = (double)((const unsigned short*)fr.depth)[p] / 1000.0;
-                    depthm[p] = d;
-                } else {
-                    d = ((const double*)fr.depth)[p];
-                }
+                const float d = DK == 0 ? (float)((const unsigned short*)fr.depth)[p] * 1e-3f
+                                        : (float)((const double*)fr.depth)[p];
                 if (CK == 0) {
                     const unsigned char* q = (const unsigned char*)fr.color + 3 * (size_t)p;
                     rgbx[p] = (unsigned)q[0] | ((unsigned)q[1] << 8) | ((unsigned)q[2] << 16);

@@ -357,17 +357,23 @@ int ensure_room(tsdf_hash* h) {
 
 // One hash integrate pass over a batch: the listed bricks (list/count from k_cull, or an
 // explicit list of skipped entries).
-void launch_integrate(tsdf_hash* h, const Batch& bt, int ck, const unsigned* list, unsigned int* count,
-                      int n_list) {
+void launch_integrate(tsdf_hash* h, const Batch& bt, int dk, int ck, const unsigned* list,
+                      unsigned int* count, int n_list) {
     Base& B = h->b;
-    const void* kern = ck == TSDF_COLOR_RGB8 ? (const void*)k_integrate<true, 0, true> : (const void*)k_integrate<true, 1, true>;
-    const unsigned grid = B.grid_for(kern);
-    if (ck == TSDF_COLOR_RGB8)
-        hipLaunchKernelGGL((k_integrate<true, 0, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
-                           B.stats, list, count, n_list);
-    else
-        hipLaunchKernelGGL((k_integrate<true, 1, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, B.pool, h->t,
-                           B.stats, list, count, n_list);
+    const unsigned grid = B.grid_for((const void*)k_integrate<true, 0, 0, true>);
+    const int sel = (dk == TSDF_DEPTH_U16_MM ? 0 : 2) | (ck == TSDF_COLOR_RGB8 ? 0 : 1);
+    switch (sel) {
+#define TSDF_LAUNCH(S, DK_, CK_)                                                                        \
+    case S:                                                                                             \
+        hipLaunchKernelGGL((k_integrate<true, DK_, CK_, true>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, \
+                           B.pool, h->t, B.stats, list, count, n_list);                                 \
+        break;
+        TSDF_LAUNCH(0, 0, 0)
+        TSDF_LAUNCH(1, 0, 1)
+        TSDF_LAUNCH(2, 1, 0)
+        TSDF_LAUNCH(3, 1, 1)
+#undef TSDF_LAUNCH
+    }
 }
 
 int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int ck,
@@ -387,7 +393,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
-        launch_integrate(h, bt, ck, (const unsigned*)B.list, B.count, 0);
+        launch_integrate(h, bt, dk, ck, (const unsigned*)B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
@@ -412,7 +418,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
                 TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
             else
                 TSDF_TRY(resize_table(h, h->t.capacity * 2));
-            launch_integrate(h, bt, ck, h->d_list, nullptr, (int)n_ov);
+            launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
             TSDF_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
             TSDF_HIP(hipGetLastError());

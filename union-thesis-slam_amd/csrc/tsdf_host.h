@@ -59,7 +59,6 @@ struct Base {
     Pool pool{};
     long long n_bricks = 0;
     float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
-    double* depthm = nullptr;  // kMaxBatch per-frame f64 metres images (u16 input)
     unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
     int pyr_H = 0, pyr_W = 0;
     unsigned* list = nullptr;   // per-batch list of (brick | frame mask << 24) kept by the cull
