@@ -1,0 +1,126 @@
+"""The N>1 path on the CPU: world_size-2 `gloo` jobs that partition the volume exactly as the GPU
+ranks do (tsdf_amd.sharding), integrate each shard with the oracle, and gather/merge the shards.
+The result must equal one unsharded oracle volume bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import load_lounge, lounge_intrinsics
+
+C1 = [[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _dense_worker(rank, world, port, out_dir):
+    import oracle as O
+    from tsdf_amd import sharding
+    dist = _init(rank, world, port)
+    vol_full_dims = O.OracleTSDFVolume(np.array(C1), 0.04)._vol_dim
+    x0, x1 = sharding.slab(rank, world, int(vol_full_dims[0]))
+    vol = O.OracleTSDFVolume(np.array(C1), 0.04, slab=(x0, x1))
+    K = lounge_intrinsics()
+    n = 0
+    for f in range(2):
+        _, depth, rgb, pose = load_lounge(f)
+        n += vol.integrate(rgb, depth, K, pose)
+    full = [sharding.gather_slabs(a, (x0, x1), int(vol_full_dims[0]))
+            for a in (vol._tsdf_vol_cpu, vol._weight_vol_cpu, vol._color_vol_cpu)]
+    tot = sharding.sum_counters({"updates": n})
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "dense.npz"), t=full[0], w=full[1], c=full[2], n=tot["updates"])
+    dist.destroy_process_group()
+
+
+def _hash_worker(rank, world, port, out_dir):
+    import oracle as O
+    from tsdf_amd import sharding
+    dist = _init(rank, world, port)
+    hv = O.OracleHashVolume(np.array(C1), 0.04)
+    K = lounge_intrinsics()
+    _, depth, rgb, pose = load_lounge(0)
+    hv.integrate(rgb, depth, K, pose)
+    # keep only the blocks this rank owns (bucket-range ownership over a 2^16-slot table)
+    X, Y, Z = (int(d) for d in hv._vol_dim)
+    bx, by, bz = np.meshgrid(np.arange(X) // 8, np.arange(Y) // 8, np.arange(Z) // 8, indexing="ij")
+    own = sharding.hash_owner(bx, by, bz, 1 << 16, world) == rank
+    t = np.where(own, hv.sdf, 1.0).astype(np.float32)
+    w = np.where(own, hv.weight, 0.0).astype(np.float32)
+    c = np.where(own, hv.color, 0.0).astype(np.float32)
+    T, W, C = sharding.merge_hash_exports(t, w, c)
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "hash.npz"), t=T, w=W, c=C, owned=int(own.sum()))
+    dist.destroy_process_group()
+
+
+def _run(fn, tmp_path, world=2):
+    mp.start_processes(fn, args=(world, _port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+
+
+def test_slab_partition_properties():
+    from tsdf_amd import sharding
+    for nx in (1, 7, 8, 100, 128, 405, 512, 1024):
+        for world in (1, 2, 3, 4, 8):
+            parts = [sharding.slab(r, world, nx) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == nx
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            if nx >= 8 * world:
+                assert all(p[0] % 8 == 0 for p in parts)
+                assert all(p[1] > p[0] for p in parts)
+
+
+def test_hash_owner_matches_oracle_keys():
+    import oracle as O
+    from tsdf_amd import sharding
+    rng = np.random.default_rng(3)
+    b = rng.integers(0, 128, size=(500, 3))
+    for bits in (64, 32):
+        home = O.hash_keys(b, 1 << 22, bits)
+        assert np.array_equal(sharding.ref_hash(b[:, 0], b[:, 1], b[:, 2], 1 << 22, bits), home)
+        assert np.array_equal(sharding.hash_owner(b[:, 0], b[:, 1], b[:, 2], 1 << 22, 8, bits), home * 8 // (1 << 22))
+
+
+def test_dense_slabs_two_ranks_gloo(tmp_path):
+    import oracle as O
+    _run(_dense_worker, tmp_path)
+    g = np.load(os.path.join(tmp_path, "dense.npz"))
+    ref = O.OracleTSDFVolume(np.array(C1), 0.04)
+    K = lounge_intrinsics()
+    n = 0
+    for f in range(2):
+        _, depth, rgb, pose = load_lounge(f)
+        n += ref.integrate(rgb, depth, K, pose)
+    assert np.array_equal(g["t"].view(np.uint32), ref._tsdf_vol_cpu.view(np.uint32))
+    assert np.array_equal(g["w"], ref._weight_vol_cpu) and np.array_equal(g["c"], ref._color_vol_cpu)
+    assert int(g["n"]) == n
+
+
+def test_hash_bucket_ranges_two_ranks_gloo(tmp_path):
+    import oracle as O
+    _run(_hash_worker, tmp_path)
+    g = np.load(os.path.join(tmp_path, "hash.npz"))
+    hv = O.OracleHashVolume(np.array(C1), 0.04)
+    _, depth, rgb, pose = load_lounge(0)
+    hv.integrate(rgb, depth, lounge_intrinsics(), pose)
+    assert np.array_equal(g["w"], hv.weight.astype(np.float32))
+    assert np.array_equal(g["c"], hv.color.astype(np.float32))
+    assert np.array_equal(g["t"], hv.sdf.astype(np.float32))
+    assert 0 < int(g["owned"]) < hv.weight.size
