@@ -10,9 +10,10 @@
 A step is one frame integrated (pyramid + fused cull/integrate kernels).  The F synthetic frames
 (tsdf_amd.scene: ray-cast room with spheres, u16 millimetre depth, RGB) are generated directly in
 HBM before timing; W warmup frames, then K timed frames issued as one asynchronous batch,
-bracketed by barrier + synchronize; the max over ranks is taken.  With N ranks each rank owns an
-x-slab of the volume and integrates every frame into it -- no data-path
-collective -- so total work is fixed: "scaling": "strong".
+bracketed by barrier + synchronize; the max over ranks is taken.  With N ranks each rank owns the
+8-voxel x-columns c with c % N == rank (cyclic column shards, DESIGN.md §6: balanced frustum
+share per rank) and integrates every frame into them -- no data-path collective -- so total work
+is fixed: "scaling": "strong".
 
 Rank 0 prints ONE JSON line.  `roofline` prices the integrate kernel by SURVEY §8(d)'s
 algorithmic bytes (24 B per updated voxel + 5 B per pixel per frame) over its HIP-event time;
@@ -145,11 +146,10 @@ def main():
 
     # ---- dense grid: this rank's x-slab of 512^3 @ 2 cm --------------------------------------
     X = int(round(ROOM / VOXEL))
-    x0, x1 = rank * X // n, (rank + 1) * X // n
     bnds = np.array([[0.0, ROOM]] * 3)
     import contextlib
     with contextlib.redirect_stdout(sys.stderr):  # the reference-style ctor prints; keep stdout JSON-only
-        vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=local, slab=(x0, x1))
+        vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=local, shard=(rank, n))
     W, Kt = args.warmup, args.steps
     run_timed(vol, depth, rgb, K, Tinv, 0, W, F, sync, barrier, False)
     dt = run_timed(vol, depth, rgb, K, Tinv, W, Kt, F, sync, barrier, not args.no_profile)
@@ -165,7 +165,7 @@ def main():
         ach = alg_bytes / kernel_s / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "tsdf::k_integrate<false,0,0> (fused cull + integrate)",
+                "kernel": "tsdf::k_integrate<HASH=false, u16 depth, rgb8, ow==1>",
                 "kernel_avg_us": round(1e6 * kernel_s / st["kernel_launches"], 2),
                 "bytes_per_launch": round(alg_bytes / st["kernel_launches"]),
                 "launches": st["kernel_launches"]}
@@ -177,7 +177,7 @@ def main():
             roof["traffic_source"] = "profiles/pmc_integrate_r01.json (separate rocprofv3 --pmc pass)"
     vf_mean = st["voxel_updates"] / Kt
     log(f"[rank {rank}] dense: {Kt} frames in {dt * 1e3:.1f} ms -> {Kt / dt:.0f} frames/s, "
-        f"V_f mean {vf_mean:.0f} ({100 * vf_mean / ((x1 - x0) * X * X):.1f}% of slab), "
+        f"V_f mean {vf_mean:.0f} ({100 * vf_mean / (len(vol.x_index) * X * X):.1f}% of shard), "
         f"kernel {st['kernel_ms']:.1f} ms over {st['kernel_launches']} launches, "
         f"bricks visited/frame {st['bricks_visited'] / Kt:.0f}, touched/frame {st['bricks_touched'] / Kt:.0f}")
     del vol
@@ -238,7 +238,7 @@ def main():
             "data": "synthetic (ray-cast 10.24 m room + spheres, u16 mm depth, RGB8; generated in HBM)",
             "config": {"workload": "config[1]: 1000 synthetic 640x480 frames into 512^3 @ 2 cm dense grid",
                        "volume": "512x512x512 @ 0.02 m", "frames_resident": F, "image": "640x480",
-                       "parallelism": f"x-slab x{n}" if n > 1 else "single GPU"},
+                       "parallelism": f"cyclic 8-voxel x-columns over {n} ranks" if n > 1 else "single GPU"},
             "mvox_updates_per_s": round(vox / dt_max / 1e6, 1),
             "mean_voxels_updated_per_frame": round(vox / Kt),
             "hash": hash_res,

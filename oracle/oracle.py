@@ -50,6 +50,10 @@ def lib():
         L.oracle_dense_integrate_slab.argtypes = [P, P, P, ctypes.c_double, ctypes.c_double, P, P, P,
                                                   P, P, ctypes.c_int, ctypes.c_int, P, P,
                                                   ctypes.c_double, P]
+        L.oracle_dense_integrate_rows.restype = ctypes.c_int64
+        L.oracle_dense_integrate_rows.argtypes = [P, P, P, P, ctypes.c_double, ctypes.c_double, P, P,
+                                                  P, P, P, ctypes.c_int, ctypes.c_int, P, P,
+                                                  ctypes.c_double, P]
         L.oracle_hash_integrate.restype = ctypes.c_int64
         L.oracle_hash_integrate.argtypes = [P, P, ctypes.c_double, ctypes.c_double, P, P, P, P,
                                             P, ctypes.c_int, ctypes.c_int, P, P, P, P]
@@ -83,15 +87,21 @@ def volume_geometry(vol_bnds, voxel_size):
 
 class OracleTSDFVolume:
     """CPU oracle with TSDFVolume's semantics (grid_fusion.py:19-320, CPU mode).  `slab` =
-    (x0, x1) keeps only that x-range of the volume (the multi-GPU partition)."""
+    (x0, x1) keeps only that x-range of the volume; `x_index` keeps the listed global x rows
+    (cyclic column shards).  Both are the multi-GPU partitions of DESIGN.md §6."""
 
-    def __init__(self, vol_bnds, voxel_size, slab=None):
+    def __init__(self, vol_bnds, voxel_size, slab=None, x_index=None):
         self._vol_bnds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
             vol_bnds, voxel_size)
         self._trunc_margin = 5 * self._voxel_size
         x0, x1 = (0, int(self._vol_dim[0])) if slab is None else slab
         self._off = np.array([x0, 0, 0], np.int64)
-        self._local_dim = np.array([x1 - x0, self._vol_dim[1], self._vol_dim[2]], np.int64)
+        self._xmap = None
+        nxl = x1 - x0
+        if x_index is not None:
+            self._xmap = np.ascontiguousarray(x_index, dtype=np.int64)
+            nxl = len(self._xmap)
+        self._local_dim = np.array([nxl, self._vol_dim[1], self._vol_dim[2]], np.int64)
         shape = tuple(int(d) for d in self._local_dim)
         self._tsdf_vol_cpu = np.ones(shape, np.float32)
         self._weight_vol_cpu = np.zeros(shape, np.float32)
@@ -105,8 +115,8 @@ class OracleTSDFVolume:
         K = np.ascontiguousarray(cam_intr, dtype=np.float64).reshape(9)
         Tinv = np.ascontiguousarray(np.linalg.inv(cam_pose), dtype=np.float64).reshape(16)
         upd = np.zeros(self._tsdf_vol_cpu.size, np.uint8) if want_mask else None
-        n = lib().oracle_dense_integrate_slab(
-            _p(self._local_dim), _p(self._off), _p(self._vol_origin), self._voxel_size, self._trunc_margin,
+        n = lib().oracle_dense_integrate_rows(
+            _p(self._local_dim), _p(self._off), _p(self._xmap), _p(self._vol_origin), self._voxel_size, self._trunc_margin,
             _p(self._tsdf_vol_cpu), _p(self._weight_vol_cpu), _p(self._color_vol_cpu),
             _p(depth), _p(col), im_h, im_w, _p(K), _p(Tinv), float(obs_weight), _p(upd))
         self.last_updated = upd

@@ -29,6 +29,7 @@
 typedef struct {
     int64_t dims[3];
     int64_t off[3]; /* global index of local voxel (0,0,0): slab sharding */
+    const int64_t* xmap; /* if set, global x of local x row (cyclic column sharding) */
     float origin[3];
     double vs, trunc;
     double fx, fy, cx, cy; /* f64(f32(K)) as cam2pix casts intr to float32 first */
@@ -40,7 +41,8 @@ typedef struct {
  * pixel with z > 0 (grid_fusion.py:273-277). */
 static inline int project(const proj_t* p, int64_t ix, int64_t iy, int64_t iz, int64_t* pix,
                           double* zout) {
-    const float px = (float)((double)p->origin[0] + p->vs * (double)(float)(ix + p->off[0]));
+    const int64_t gx = p->xmap ? p->xmap[ix] : ix + p->off[0];
+    const float px = (float)((double)p->origin[0] + p->vs * (double)(float)gx);
     const float py = (float)((double)p->origin[1] + p->vs * (double)(float)(iy + p->off[1]));
     const float pz = (float)((double)p->origin[2] + p->vs * (double)(float)(iz + p->off[2]));
     const double* T = p->T;
@@ -62,6 +64,7 @@ static void fill_proj(proj_t* p, const int64_t* dims, const float* origin, doubl
                       double trunc, const double* K, const double* Tinv, int H, int W) {
     memcpy(p->dims, dims, sizeof(p->dims));
     memset(p->off, 0, sizeof(p->off));
+    p->xmap = NULL;
     memcpy(p->origin, origin, sizeof(p->origin));
     p->vs = vs;
     p->trunc = trunc;
@@ -77,13 +80,15 @@ static void fill_proj(proj_t* p, const int64_t* dims, const float* origin, doubl
 /* Dense grid integrate (grid_fusion.py:214-314, CPU branch).  State is C-order (X,Y,Z) f32.
  * depth: H*W float64 metres.  colour: H*W float32 folded B*65536+G*256+R (grid_fusion.py:232).
  * Returns the number of voxels updated; if `upd` is non-NULL, upd[i] = 1 for updated voxels. */
-int64_t oracle_dense_integrate_slab(const int64_t* dims, const int64_t* off, const float* origin,
-                                    double vs, double trunc, float* tsdf, float* weight, float* color,
-                                    const double* depth, const float* color_im, int H, int W,
-                                    const double* K, const double* Tinv, double ow, uint8_t* upd) {
+int64_t oracle_dense_integrate_rows(const int64_t* dims, const int64_t* off, const int64_t* xmap,
+                                    const float* origin, double vs, double trunc, float* tsdf,
+                                    float* weight, float* color, const double* depth,
+                                    const float* color_im, int H, int W, const double* K,
+                                    const double* Tinv, double ow, uint8_t* upd) {
     proj_t p;
     fill_proj(&p, dims, origin, vs, trunc, K, Tinv, H, W);
     if (off) memcpy(p.off, off, sizeof(p.off));
+    p.xmap = xmap;
     const float ow32 = (float)ow; /* NumPy weak-scalar: Python float * f32 array stays f32 */
     int64_t n = 0;
     int64_t i = 0;
@@ -124,6 +129,14 @@ int64_t oracle_dense_integrate_slab(const int64_t* dims, const int64_t* off, con
                 ++n;
             }
     return n;
+}
+
+int64_t oracle_dense_integrate_slab(const int64_t* dims, const int64_t* off, const float* origin,
+                                    double vs, double trunc, float* tsdf, float* weight, float* color,
+                                    const double* depth, const float* color_im, int H, int W,
+                                    const double* K, const double* Tinv, double ow, uint8_t* upd) {
+    return oracle_dense_integrate_rows(dims, off, NULL, origin, vs, trunc, tsdf, weight, color, depth,
+                                       color_im, H, W, K, Tinv, ow, upd);
 }
 
 int64_t oracle_dense_integrate(const int64_t* dims, const float* origin, double vs, double trunc,

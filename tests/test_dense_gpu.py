@@ -210,6 +210,37 @@ def test_slab_shards_reassemble_bit_exact(gf):
         assert _same(F[k], np.concatenate([p[k] for p in P], axis=0))
 
 
+@pytest.mark.parametrize("world", [3, 8])
+def test_cyclic_column_shards_reassemble_bit_exact(gf, world):
+    """Cyclic brick-column sharding (tsdf_dense_create_shard, the bench's multi-GPU layout):
+    every shard equals the unsharded volume's rows at its global x, including a ragged last
+    column (X = 101 is not a multiple of 8), for both single-frame and batched integrate."""
+    from tsdf_amd import sharding
+    bnds = np.array([[-2.56, 1.48], [-2.56, 2.56], [0.0, 5.12]])  # 101 x 128 x 128 @ 4 cm
+    K = lounge_intrinsics()
+    full = O.OracleTSDFVolume(bnds.copy(), 0.04)
+    X = int(full._vol_dim[0])
+    assert X == 101
+    parts = [gf.TSDFVolume(bnds.copy(), 0.04, shard=(r, world)) for r in range(world)]
+    frames = [load_lounge(f) for f in range(3)]
+    for _, depth, rgb, pose in frames:
+        full.integrate(rgb, depth, K, pose)
+    for p in parts:
+        p.integrate(frames[0][2], frames[0][1], K, frames[0][3])
+        d = np.stack([fr[1] for fr in frames[1:]])
+        c = np.stack([fr[2] for fr in frames[1:]])
+        p.integrate_batch(d, c, K, np.linalg.inv(np.stack([fr[3] for fr in frames[1:]])))
+    seen = np.zeros(X, int)
+    for r, p in enumerate(parts):
+        xi = sharding.columns(r, world, X)
+        assert np.array_equal(p.x_index, xi)
+        seen[xi] += 1
+        T, W, C = p.get_state()
+        assert _same(T, full._tsdf_vol_cpu[xi]) and _same(W, full._weight_vol_cpu[xi])
+        assert _same(C, full._color_vol_cpu[xi])
+    assert (seen == 1).all()
+
+
 def test_long_batch_without_host_sync_matches_oracle(gf):
     """24 frames in one async batch (no host synchronisation between frames, as in the bench):
     cross-kernel visibility of the brick state must hold whatever XCD a brick lands on."""

@@ -29,23 +29,28 @@ def _init(rank, world, port):
     return dist
 
 
-def _dense_worker(rank, world, port, out_dir):
+def _dense_worker(rank, world, port, out_dir, cyclic=False):
     import oracle as O
     from tsdf_amd import sharding
     dist = _init(rank, world, port)
-    vol_full_dims = O.OracleTSDFVolume(np.array(C1), 0.04)._vol_dim
-    x0, x1 = sharding.slab(rank, world, int(vol_full_dims[0]))
-    vol = O.OracleTSDFVolume(np.array(C1), 0.04, slab=(x0, x1))
+    nx = int(O.OracleTSDFVolume(np.array(C1), 0.04)._vol_dim[0])
+    if cyclic:
+        xi = sharding.columns(rank, world, nx)
+        vol = O.OracleTSDFVolume(np.array(C1), 0.04, x_index=xi)
+    else:
+        x0, x1 = sharding.slab(rank, world, nx)
+        xi = np.arange(x0, x1)
+        vol = O.OracleTSDFVolume(np.array(C1), 0.04, slab=(x0, x1))
     K = lounge_intrinsics()
     n = 0
     for f in range(2):
         _, depth, rgb, pose = load_lounge(f)
         n += vol.integrate(rgb, depth, K, pose)
-    full = [sharding.gather_slabs(a, (x0, x1), int(vol_full_dims[0]))
+    full = [sharding.gather_rows(a, xi, nx)
             for a in (vol._tsdf_vol_cpu, vol._weight_vol_cpu, vol._color_vol_cpu)]
     tot = sharding.sum_counters({"updates": n})
     if rank == 0:
-        np.savez(os.path.join(out_dir, "dense.npz"), t=full[0], w=full[1], c=full[2], n=tot["updates"])
+        np.savez(os.path.join(out_dir, f"dense{int(cyclic)}.npz"), t=full[0], w=full[1], c=full[2], n=tot["updates"])
     dist.destroy_process_group()
 
 
@@ -70,6 +75,10 @@ def _hash_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _cyclic_worker(rank, world, port, out_dir):
+    _dense_worker(rank, world, port, out_dir, cyclic=True)
+
+
 def _run(fn, tmp_path, world=2):
     mp.start_processes(fn, args=(world, _port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
@@ -87,6 +96,18 @@ def test_slab_partition_properties():
                 assert all(p[1] > p[0] for p in parts)
 
 
+def test_cyclic_columns_partition():
+    from tsdf_amd import sharding
+    for nx in (16, 101, 128, 512, 1000):
+        for world in (1, 2, 3, 8):
+            if -(-nx // 8) < world:
+                continue
+            cols = [sharding.columns(r, world, nx) for r in range(world)]
+            allx = np.sort(np.concatenate(cols))
+            assert np.array_equal(allx, np.arange(nx))
+            assert max(len(c) for c in cols) - min(len(c) for c in cols) <= 8
+
+
 def test_hash_owner_matches_oracle_keys():
     import oracle as O
     from tsdf_amd import sharding
@@ -98,10 +119,11 @@ def test_hash_owner_matches_oracle_keys():
         assert np.array_equal(sharding.hash_owner(b[:, 0], b[:, 1], b[:, 2], 1 << 22, 8, bits), home * 8 // (1 << 22))
 
 
-def test_dense_slabs_two_ranks_gloo(tmp_path):
+@pytest.mark.parametrize("cyclic", [False, True])
+def test_dense_slabs_two_ranks_gloo(tmp_path, cyclic):
     import oracle as O
-    _run(_dense_worker, tmp_path)
-    g = np.load(os.path.join(tmp_path, "dense.npz"))
+    _run(_cyclic_worker if cyclic else _dense_worker, tmp_path)
+    g = np.load(os.path.join(tmp_path, f"dense{int(cyclic)}.npz"))
     ref = O.OracleTSDFVolume(np.array(C1), 0.04)
     K = lounge_intrinsics()
     n = 0

@@ -12,6 +12,11 @@ rc=$?; echo "smoke rc=$rc" >> gpurun_out/smoke.log
 timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc" >> gpurun_out/bench.err
 [ $rc -eq 0 ] || exit $rc
+if [ -n "${SCALE:-}" ]; then
+  timeout -k 10 600 python tools/scaling_sim.py > gpurun_out/scaling_sim.json 2> gpurun_out/scaling_sim.err
+  rc=$?; echo "scaling rc=$rc" >> gpurun_out/scaling_sim.err
+  [ $rc -eq 0 ] || exit $rc
+fi
 if [ -n "${PROF:-}" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run --output-format csv -- python "$R/bench.py" --steps 1000 --warmup 50 --no-cpu --no-profile > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err"

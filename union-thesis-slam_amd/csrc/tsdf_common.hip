@@ -110,6 +110,7 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     if (!(vs > 0.0) || !(trunc > 0.0)) return set_error(TSDF_E_ARG, "voxel_size and trunc must be > 0");
     vol.vs = vs;
     vol.trunc = trunc;
+    vol.xstride = kBrickEdge;
     vol.shard = 0;
     vol.n_shards = 1;
     n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];

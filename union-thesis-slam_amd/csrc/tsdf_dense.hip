@@ -117,12 +117,17 @@ int dense_xfer(tsdf_dense* h, float* tsdf_, float* weight_, float* color_, bool 
 
 extern "C" {
 
-int tsdf_dense_create(const int64_t dims[3], const int64_t index_offset[3], const float origin[3],
-                      double voxel_size, double trunc, int device, tsdf_dense_t** out) {
-    if (!dims || !origin || !out) return set_error(TSDF_E_ARG, "null pointer");
+static int dense_create(const int64_t dims[3], const int64_t index_offset[3], int xstride,
+                        const float origin[3], double voxel_size, double trunc, int device,
+                        tsdf_dense_t** out) {
     *out = nullptr;
     tsdf_dense* h = new tsdf_dense();
     int r = h->b.init(device, dims, index_offset, origin, voxel_size, trunc);
+    if (r == TSDF_OK) {
+        h->b.vol.xstride = xstride;
+        const int64_t gx_max = (int64_t)h->b.vol.off[0] + (int64_t)(h->b.vol.nb[0] - 1) * xstride + kBrickEdge;
+        if (gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
+    }
     if (r == TSDF_OK) {
         const size_t n = (size_t)h->b.n_bricks * kBrickVox * sizeof(float);
         hipError_t e = hipMalloc(&h->b.pool.tsdf, n);
@@ -141,6 +146,30 @@ int tsdf_dense_create(const int64_t dims[3], const int64_t index_offset[3], cons
     }
     *out = h;
     return TSDF_OK;
+}
+
+int tsdf_dense_create(const int64_t dims[3], const int64_t index_offset[3], const float origin[3],
+                      double voxel_size, double trunc, int device, tsdf_dense_t** out) {
+    if (!dims || !origin || !out) return set_error(TSDF_E_ARG, "null pointer");
+    return dense_create(dims, index_offset, kBrickEdge, origin, voxel_size, trunc, device, out);
+}
+
+int tsdf_dense_create_shard(const int64_t global_dims[3], int shard, int n_shards,
+                            const float origin[3], double voxel_size, double trunc, int device,
+                            tsdf_dense_t** out) {
+    if (!global_dims || !origin || !out) return set_error(TSDF_E_ARG, "null pointer");
+    *out = nullptr;
+    if (n_shards < 1 || shard < 0 || shard >= n_shards)
+        return set_error(TSDF_E_ARG, "shard %d of %d", shard, n_shards);
+    const int64_t X = global_dims[0];
+    const int64_t cols = (X + kBrickEdge - 1) / kBrickEdge;
+    if (X <= 0 || shard >= cols) return set_error(TSDF_E_ARG, "shard %d owns no x-column of %lld voxels", shard, (long long)X);
+    const int64_t mine = (cols - 1 - shard) / n_shards + 1;  // columns shard, shard+n, ...
+    const int64_t last = shard + (mine - 1) * n_shards;
+    const int64_t last_w = (last == cols - 1) ? X - last * kBrickEdge : kBrickEdge;
+    const int64_t dims[3] = {(mine - 1) * kBrickEdge + last_w, global_dims[1], global_dims[2]};
+    const int64_t off[3] = {(int64_t)shard * kBrickEdge, 0, 0};
+    return dense_create(dims, off, kBrickEdge * n_shards, origin, voxel_size, trunc, device, out);
 }
 
 int tsdf_dense_destroy(tsdf_dense_t* h) {

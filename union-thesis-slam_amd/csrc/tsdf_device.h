@@ -32,6 +32,8 @@ enum Stat { ST_VOXELS = 0, ST_VISITED, ST_TOUCHED, ST_ALLOC, ST_PROBE, ST_LOOKUP
 struct Vol {
     int dims[3];    // voxels of this shard
     int off[3];     // global voxel index of local (0,0,0)
+    int xstride;    // global x distance between consecutive local brick columns (8: contiguous;
+                    // 8*S: cyclic brick-column sharding over S ranks)
     int nb[3];      // bricks per axis (ceil(dims/8))
     int shard, n_shards;
     float origin[3];
@@ -155,7 +157,8 @@ __device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz) {
     for (int a = 0; a < 3; ++a) {
         const int lo = bb[a] * kBrickEdge;
         const int hi = min(lo + kBrickEdge - 1, v.dims[a] - 1);
-        r.p0[a] = (double)v.origin[a] + v.vs * (double)(lo + v.off[a]);
+        const int g = (a == 0) ? bb[0] * v.xstride : lo;  // global index of the low corner
+        r.p0[a] = (double)v.origin[a] + v.vs * (double)(g + v.off[a]);
         r.ext[a] = (float)(v.vs * (double)(hi - lo));
         r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(hi - lo));
     }
@@ -359,7 +362,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const bool col_in = lx < v.dims[0] && ly < v.dims[1];
     const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge);
     // vox2world (grid_fusion.py:170-181); lanes 0..7 compute the brick's 8 z coordinates
-    const double px = vox_world(v.origin[0], v.vs, v.off[0] + lx);
+    const double px = vox_world(v.origin[0], v.vs, v.off[0] + bx * v.xstride + (lane >> 3));
     const double py = vox_world(v.origin[1], v.vs, v.off[1] + ly);
     const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));
 

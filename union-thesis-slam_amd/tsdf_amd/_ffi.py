@@ -67,6 +67,7 @@ _D = ctypes.c_double
 SIGNATURES = {
     "tsdf_device_count": [_P],
     "tsdf_dense_create": [_P, _P, _P, _D, _D, _I, _P],
+    "tsdf_dense_create_shard": [_P, _I, _I, _P, _D, _D, _I, _P],
     "tsdf_dense_destroy": [_P],
     "tsdf_dense_reset": [_P],
     "tsdf_dense_integrate": [_P, _P, _I, _P, _I, _I, _I, _P, _P, _D, _I],

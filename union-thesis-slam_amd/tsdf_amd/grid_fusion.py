@@ -17,7 +17,7 @@ import ctypes
 
 import numpy as np
 
-from . import _ffi
+from . import _ffi, sharding
 
 
 def volume_geometry(vol_bnds, voxel_size):
@@ -68,9 +68,11 @@ class TSDFVolume:
       use_gpu: accepted for signature compatibility; the volume always lives in HBM.
     Extra keyword-only args (slab sharding):
       device: HIP device index.  slab: (x_begin, x_end) voxel range of this shard along x.
+      shard: (rank, world) cyclic brick-column shard (sharding.columns) -- the bench's layout.
+      `x_index` holds the global x of every local x row either way.
     """
 
-    def __init__(self, vol_bnds, voxel_size, use_gpu=True, *, device=0, slab=None):
+    def __init__(self, vol_bnds, voxel_size, use_gpu=True, *, device=0, slab=None, shard=None):
         print("Initializing voxel grids ... ")
         self._vol_bnds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
             vol_bnds, voxel_size)
@@ -81,17 +83,28 @@ class TSDFVolume:
             self._vol_dim[0] * self._vol_dim[1] * self._vol_dim[2]))
         self.gpu_mode = True
         self.device = int(device)
-        x0, x1 = (0, int(self._vol_dim[0])) if slab is None else (int(slab[0]), int(slab[1]))
-        if not (0 <= x0 < x1 <= int(self._vol_dim[0])):
-            raise ValueError(f"slab {slab} outside [0, {self._vol_dim[0]})")
-        self.slab = (x0, x1)
-        self._local_dim = np.array([x1 - x0, self._vol_dim[1], self._vol_dim[2]], np.int64)
-        dims = np.ascontiguousarray(self._local_dim, dtype=np.int64)
-        off = np.array([x0, 0, 0], np.int64)
+        origin = np.ascontiguousarray(self._vol_origin, dtype=np.float32)
         h = ctypes.c_void_p()
-        _ffi.call("tsdf_dense_create", _ffi.ptr(dims), _ffi.ptr(off),
-                  _ffi.ptr(np.ascontiguousarray(self._vol_origin, dtype=np.float32)),
-                  self._voxel_size, float(self._trunc_margin), self.device, ctypes.byref(h))
+        if shard is not None:
+            if slab is not None:
+                raise ValueError("give slab or shard, not both")
+            rank, world = int(shard[0]), int(shard[1])
+            self.x_index = sharding.columns(rank, world, int(self._vol_dim[0]))
+            self.slab = None
+            gdims = np.ascontiguousarray(self._vol_dim, dtype=np.int64)
+            _ffi.call("tsdf_dense_create_shard", _ffi.ptr(gdims), rank, world, _ffi.ptr(origin),
+                      self._voxel_size, float(self._trunc_margin), self.device, ctypes.byref(h))
+        else:
+            x0, x1 = (0, int(self._vol_dim[0])) if slab is None else (int(slab[0]), int(slab[1]))
+            if not (0 <= x0 < x1 <= int(self._vol_dim[0])):
+                raise ValueError(f"slab {slab} outside [0, {self._vol_dim[0]})")
+            self.slab = (x0, x1)
+            self.x_index = np.arange(x0, x1, dtype=np.int64)
+            dims = np.array([x1 - x0, self._vol_dim[1], self._vol_dim[2]], np.int64)
+            off = np.array([x0, 0, 0], np.int64)
+            _ffi.call("tsdf_dense_create", _ffi.ptr(dims), _ffi.ptr(off), _ffi.ptr(origin),
+                      self._voxel_size, float(self._trunc_margin), self.device, ctypes.byref(h))
+        self._local_dim = np.array([len(self.x_index), self._vol_dim[1], self._vol_dim[2]], np.int64)
         self._h = h
 
     # ------------------------------------------------------------------ reference API

@@ -34,6 +34,19 @@ def slab(rank: int, world: int, nx: int, align: int = BRICK):
     return rank * nx // world, (rank + 1) * nx // world
 
 
+def columns(rank: int, world: int, nx: int):
+    """Global x indices owned by `rank` under cyclic brick-column sharding (the layout
+    tsdf_dense_create_shard builds): the 8-voxel x-columns c with c % world == rank, in order.
+    Every rank then sees a similar share of each frame's frustum, unlike contiguous slabs."""
+    if not (0 <= rank < world):
+        raise ValueError(f"rank {rank} outside world {world}")
+    x = np.arange(nx, dtype=np.int64)
+    own = x[(x // BRICK) % world == rank]
+    if own.size == 0:
+        raise ValueError(f"rank {rank} of {world} owns no 8-voxel column of {nx}")
+    return own
+
+
 def ref_hash(x, y, z, n: int, int_bits: int = 64):
     """hash_function (hash_fusion.py:182-190) on integer arrays: int64 or wrapping-int32 mode."""
     x, y, z = (np.asarray(a, dtype=np.int64) for a in (x, y, z))
@@ -55,16 +68,27 @@ def hash_owner(bx, by, bz, capacity: int, n_shards: int, int_bits: int = 64):
 
 def gather_slabs(local: np.ndarray, x_range, nx: int, group=None, dst: int = 0):
     """Assemble x-slabs of an (x, Y, Z) array on rank `dst` (None elsewhere)."""
+    return gather_rows(local, np.arange(x_range[0], x_range[1], dtype=np.int64), nx, group, dst)
+
+
+def gather_rows(local: np.ndarray, x_index, nx: int, group=None, dst: int = 0):
+    """Assemble the x rows of an (x, Y, Z) array, local row i being global row x_index[i]
+    (slabs or cyclic columns), on rank `dst` (None elsewhere)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    x_index = np.asarray(x_index, dtype=np.int64)
+    if len(x_index) != local.shape[0]:
+        raise ValueError("x_index length differs from the local x extent")
     t = torch.from_numpy(np.ascontiguousarray(local)).reshape(-1)
-    meta = torch.tensor([x_range[0], x_range[1], t.numel()], dtype=torch.int64)
-    metas = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group)
-    n_max = int(max(int(m[2]) for m in metas))
+    rows = torch.full((nx,), -1, dtype=torch.int64)
+    rows[: len(x_index)] = torch.from_numpy(x_index)
+    n_rows = [torch.zeros(nx, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(n_rows, rows, group=group)
+    row = int(np.prod(local.shape[1:], dtype=np.int64))
+    n_max = max(int((r >= 0).sum()) for r in n_rows) * row
     buf = torch.zeros(n_max, dtype=t.dtype)
     buf[: t.numel()] = t
     parts = [torch.zeros(n_max, dtype=t.dtype) for _ in range(world)]
@@ -72,9 +96,14 @@ def gather_slabs(local: np.ndarray, x_range, nx: int, group=None, dst: int = 0):
     if rank != dst:
         return None
     out = np.empty((nx,) + local.shape[1:], dtype=local.dtype)
-    for m, p in zip(metas, parts):
-        x0, x1, n = (int(v) for v in m)
-        out[x0:x1] = p[:n].numpy().reshape((x1 - x0,) + local.shape[1:])
+    seen = np.zeros(nx, dtype=np.int64)
+    for r_idx, p in zip(n_rows, parts):
+        xi = r_idx.numpy()
+        xi = xi[xi >= 0]
+        out[xi] = p[: len(xi) * row].numpy().reshape((len(xi),) + local.shape[1:])
+        seen[xi] += 1
+    if not (seen == 1).all():
+        raise RuntimeError("x rows missing or owned twice across ranks")
     return out
 
 
