@@ -83,3 +83,24 @@ def test_host_encoding_duties():
     b = np.array([[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]])
     _, dims, origin, vs = volume_geometry(b, 0.04)
     assert list(dims) == [128, 128, 128] and origin.dtype == np.float32
+
+
+def test_frame_stack_kinds_follow_dtypes():
+    """integrate_batch never reinterprets host memory: kinds come from the dtypes and an
+    explicit kind that disagrees is an error (no GPU needed)."""
+    import numpy as np
+    from tsdf_amd import _ffi
+    from tsdf_amd.grid_fusion import frame_stack
+    d16 = np.zeros((2, 4, 5), np.uint16)
+    d64 = np.zeros((2, 4, 5), np.float64)
+    rgb = np.zeros((2, 4, 5, 3), np.uint8)
+    fold = np.zeros((2, 4, 5), np.float32)
+    assert frame_stack(d16, None, rgb, None, False)[1::2] == (_ffi.DEPTH_U16_MM, _ffi.COLOR_RGB8)
+    assert frame_stack(d64, None, fold, None, False)[1::2] == (_ffi.DEPTH_F64_M, _ffi.COLOR_F32)
+    with pytest.raises(ValueError):
+        frame_stack(d64, _ffi.DEPTH_U16_MM, rgb, None, False)
+    with pytest.raises(ValueError):
+        frame_stack(d64.astype(np.float32), None, rgb, None, False)
+    with pytest.raises(ValueError):
+        frame_stack(d16, None, rgb[:1], None, False)
+    assert frame_stack(123, None, 456, None, True) == (123, _ffi.DEPTH_U16_MM, 456, _ffi.COLOR_RGB8)

@@ -31,3 +31,13 @@ def test_frustum_planes_contain_the_valid_pixel_range():
     x, y = (u - cx) * z / fx, (v - cy) * z / fy
     for a, b, c, e in cam:
         assert (a * x + b * y + c * z + e >= 0).all()
+
+
+def test_markstein_quotient_matches_ieee_division(tmp_path):
+    """tsdf_device.h div_rn (RN(1/b) + one FMA correction) must equal a / b on the operand
+    ranges of the integrate kernels: diff / trunc and (w*t + dist) / (w + 1) for w < 4096."""
+    exe = os.path.join(tmp_path, "cm")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(REPO, "tools", "check_markstein.c"),
+                    "-o", exe, "-lm"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0 and "mismatches 0" in out.stdout, out.stdout

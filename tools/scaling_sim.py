@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--only", default=None, help="W:R -- time only rank R of world W (for profiling)")
     a = ap.parse_args()
     import torch
     from tsdf_amd import grid_fusion, scene, sharding
@@ -59,6 +60,14 @@ def main():
         return time.perf_counter() - t0
 
     out = {}
+    if a.only:
+        world, r = (int(x) for x in a.only.split(":"))
+        with contextlib.redirect_stdout(sys.stderr):
+            vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(r, world))
+        timed(vol, 0, a.warmup)
+        t = timed(vol, a.warmup, a.steps)
+        print(json.dumps({"only": a.only, "fps": round(a.steps / t, 1)}))
+        return
     for world in [int(w) for w in a.worlds.split(",")]:
         for mode in ("slab", "cyclic"):
             if world == 1 and mode == "cyclic":

@@ -110,7 +110,9 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     if (!(vs > 0.0) || !(trunc > 0.0)) return set_error(TSDF_E_ARG, "voxel_size and trunc must be > 0");
     vol.vs = vs;
     vol.trunc = trunc;
+    vol.rtrunc = 1.0 / trunc;  // IEEE division: RN(1/trunc)
     vol.xstride = kBrickEdge;
+    vol.sb[0] = vol.sb[1] = vol.sb[2] = 2;  // 4x4x4-brick superbricks
     vol.shard = 0;
     vol.n_shards = 1;
     n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];
@@ -134,6 +136,7 @@ int Base::ensure_pyr(int H, int W) {
         pyr = nullptr;
         rgbx = nullptr;
     }
+
     lay = pyr_layout(H, W);
     TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total * kMaxBatch));
     TSDF_HIP(hipMalloc(&rgbx, sizeof(unsigned) * (size_t)H * W * kMaxBatch));
@@ -218,6 +221,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->color = c + cbytes * i;
         fr->rgbx = rgbx + npx * i;
         fr->pyr = pyr + (size_t)lay.total * i;
+
         frustum_planes(fr, T, W, H);
         for (int L = 0; L <= kPyrLevels; ++L) {
             fr->pyr_off[L] = lay.off[L];
@@ -299,6 +303,7 @@ void Base::release() {
     prof.release();
     if (pyr) (void)hipFree(pyr);
     if (rgbx) (void)hipFree(rgbx);
+
     if (list) (void)hipFree(list);
     if (count) (void)hipFree(count);
     if (stats) (void)hipFree(stats);

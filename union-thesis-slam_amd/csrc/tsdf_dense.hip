@@ -44,14 +44,14 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
     const Table no_table{};
-    const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    const unsigned cull_grid = B.cull_grid();
     const unsigned grid = B.grid_for((const void*)k_integrate<false, 0, 0, false>);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
         TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, ow, 1.0, flags, f0, n));
         TSDF_TRY(B.launch_prep(bt, dk, ck, W, H));
-        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, bt, no_table,
+        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, no_table,
                            B.list, B.count, B.stats);
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
@@ -125,6 +125,10 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
     int r = h->b.init(device, dims, index_offset, origin, voxel_size, trunc);
     if (r == TSDF_OK) {
         h->b.vol.xstride = xstride;
+        if (xstride > kBrickEdge) {  // cyclic shard: superbricks one column wide, 8x8 in y, z
+            h->b.vol.sb[0] = 0;
+            h->b.vol.sb[1] = h->b.vol.sb[2] = 3;
+        }
         const int64_t gx_max = (int64_t)h->b.vol.off[0] + (int64_t)(h->b.vol.nb[0] - 1) * xstride + kBrickEdge;
         if (gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
     }

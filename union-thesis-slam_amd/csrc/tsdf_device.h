@@ -34,10 +34,12 @@ struct Vol {
     int off[3];     // global voxel index of local (0,0,0)
     int xstride;    // global x distance between consecutive local brick columns (8: contiguous;
                     // 8*S: cyclic brick-column sharding over S ranks)
+    int sb[3];      // log2 superbrick edge in bricks per axis (sum 6: one wave = 64 bricks)
     int nb[3];      // bricks per axis (ceil(dims/8))
     int shard, n_shards;
     float origin[3];
     double vs, trunc;
+    double rtrunc;  // RN(1 / trunc), from the host's IEEE division (Markstein quotient, below)
 };
 
 // Per-frame constants (by value).
@@ -61,6 +63,12 @@ struct Frame {
 // updates are still applied frame by frame, in order, so results are those of one-by-one
 // integration; the brick state is read and written once per batch instead of once per frame).
 constexpr int kMaxBatch = 8;
+constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
+
+// w is an integer small enough that w + kMaxBatch indexes the reciprocal table
+__device__ inline bool small_int(float w) {
+    return w >= 0.0f && w < (float)(kRcpTab - kMaxBatch - 1) && w == truncf(w);
+}
 struct Batch {
     Frame f[kMaxBatch];
     int n;
@@ -150,17 +158,22 @@ struct BrickBox {
     float rad;     // its half diagonal + 0.1 mm
 };
 
-__device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz) {
-    const int bb[3] = {bx, by, bz};
+// Box of the voxel centres of bricks [b, b + n) per axis (n = 1: one brick; larger: a superbrick,
+// whose x extent spans the gaps between a cyclic shard's columns -- a superset, fine for culling).
+__device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz, int nx = 1, int ny = 1,
+                                     int nz = 1) {
+    const int bb[3] = {bx, by, bz}, nn[3] = {nx, ny, nz};
     BrickBox r;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const int lo = bb[a] * kBrickEdge;
-        const int hi = min(lo + kBrickEdge - 1, v.dims[a] - 1);
-        const int g = (a == 0) ? bb[0] * v.xstride : lo;  // global index of the low corner
-        r.p0[a] = (double)v.origin[a] + v.vs * (double)(g + v.off[a]);
-        r.ext[a] = (float)(v.vs * (double)(hi - lo));
-        r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(hi - lo));
+        const int hi = min(lo + nn[a] * kBrickEdge - 1, v.dims[a] - 1);
+        // global indices of the low / high corner (x: local brick column -> global column)
+        const int glo = (a == 0) ? bb[0] * v.xstride : lo;
+        const int ghi = (a == 0) ? (hi >> 3) * v.xstride + (hi & 7) : hi;
+        r.p0[a] = (double)v.origin[a] + v.vs * (double)(glo + v.off[a]);
+        r.ext[a] = (float)(v.vs * (double)(ghi - glo));
+        r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(ghi - glo));
     }
     r.rad = 0.5f * sqrtf(r.ext[0] * r.ext[0] + r.ext[1] * r.ext[1] + r.ext[2] * r.ext[2]) + 1e-4f;
     return r;
@@ -206,15 +219,22 @@ __device__ inline bool cull_brick(const Vol& v, const Frame& fr, const BrickBox&
         u0 = (int)fmaxf(fu0, 0.0f); u1 = (int)fminf(fu1, (float)(fr.W - 1));
         v0 = (int)fmaxf(fv0, 0.0f); v1 = (int)fminf(fv1, (float)(fr.H - 1));
     }
-    // max depth over the bbox from the smallest pyramid level where it spans <= 4x4 texels
+    // max depth over the bbox from the smallest pyramid level where it spans <= 4x4 texels (16
+    // independent predicated loads); a bbox wider than that at the coarsest level (a box very
+    // close to the camera) is kept without a depth test
     int L = 1;
     while (L < kPyrLevels && (((u1 >> L) - (u0 >> L)) > 3 || ((v1 >> L) - (v0 >> L)) > 3)) ++L;
     const float need = zmin - (float)v.trunc - 1e-3f;
+    const int tx0 = u0 >> L, tx1 = u1 >> L, ty0 = v0 >> L, ty1 = v1 >> L;
+    if (tx1 - tx0 > 3 || ty1 - ty0 > 3) return true;
     const float* lvl = fr.pyr + fr.pyr_off[L];
     const int wl = fr.pyr_w[L];
     float dmax = 0.0f;
-    for (int ty = v0 >> L; ty <= (v1 >> L); ++ty)
-        for (int tx = u0 >> L; tx <= (u1 >> L); ++tx) dmax = fmaxf(dmax, lvl[ty * wl + tx]);
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx)
+            if (ty0 + dy <= ty1 && tx0 + dx <= tx1) dmax = fmaxf(dmax, lvl[(ty0 + dy) * wl + tx0 + dx]);
     return dmax > 0.0f && dmax >= need;
 }
 
@@ -324,6 +344,17 @@ __device__ inline double depth_m(const Frame& fr, int p) {
 // can be valid (|u| < 1e3).  Steps whose u is within 1e-9 px of a rounding boundary (or not
 // finite) are recomputed with the reference's own division.
 // ---------------------------------------------------------------------------------------------
+// RN(a / b) given y = RN(1 / b): Markstein's correction step.  q0 = RN(a*y) is within 1 ulp
+// of a/b, r = a - b*q0 is exact with an FMA, and RN(q0 + r*y) is then the correctly rounded
+// quotient (Markstein 1990; Muller et al., Handbook of Floating-Point Arithmetic, "Markstein's
+// theorem"), barring under/overflow, which the TSDF ranges exclude.  tests/test_numerics_cpu.py
+// re-checks it on the kernels' operand ranges.
+__device__ inline double div_rn(double a, double b, double y) {
+    const double q0 = a * y;
+    const double r = fma(-q0, b, a);
+    return fma(r, y, q0);
+}
+
 __device__ inline double refined_rcp(double z) {
     const double y = __builtin_amdgcn_rcp(z);
     return fma(y, fma(-z, y, 1.0), y);
@@ -348,7 +379,8 @@ __device__ inline double readlane_f64(double x, int l) {
 // ---------------------------------------------------------------------------------------------
 template <bool HASH, int DK, int CK, bool OW1>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
-                                       const Table& tab, unsigned entry, unsigned long long* s_stat) {
+                                       const Table& tab, unsigned entry, unsigned long long* s_stat,
+                                       const double* s_rcp) {
     const int lane = lane_id();
     const int b = (int)(entry & 0xFFFFFFu);
     const unsigned fmask = entry >> 24;
@@ -379,6 +411,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     long long blk = -1;
     bool is_new = false;
     int nupd = 0;
+    bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
 
     for (int fi = 0; fi < bt.n; ++fi) {
         if (!((fmask >> fi) & 1u)) continue;
@@ -441,7 +474,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         for (int k = 0; k < kBrickEdge; ++k) {
             const double diff = dep[k] - zc[k];
             const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
-            const double dd = diff / v.trunc;
+            const double dd = div_rn(diff, v.trunc, v.rtrunc);
             dist[k] = dd > 1.0 ? 1.0 : dd;  // np.minimum(1, .)
             vmask |= (unsigned)ok << k;
         }
@@ -482,6 +515,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float4 T = *(const float4*)(pool.tsdf + base);
             const float4 C = *(const float4*)(pool.color + base);
             ws[0] = W.x; ws[1] = W.y; ws[2] = W.z; ws[3] = W.w;
+            w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
             ts[0] = T.x; ts[1] = T.y; ts[2] = T.z; ts[3] = T.w;
             cs[0] = C.x; cs[1] = C.y; cs[2] = C.z; cs[3] = C.w;
         }
@@ -490,6 +524,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float4 T = *(const float4*)(pool.tsdf + base + 4);
             const float4 C = *(const float4*)(pool.color + base + 4);
             ws[4] = W.x; ws[5] = W.y; ws[6] = W.z; ws[7] = W.w;
+            w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
             ts[4] = T.x; ts[5] = T.y; ts[6] = T.z; ts[7] = T.w;
             cs[4] = C.x; cs[5] = C.y; cs[6] = C.z; cs[7] = C.w;
         }
@@ -502,16 +537,32 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const int p = ((vmask >> k) & 1u) ? pix[k] : 0;
             cpx[k] = (CK == 0) ? fr.rgbx[p] : __float_as_uint(((const float*)fr.color)[p]);
         }
-        // phase 5: update in registers, straight-line; invalid steps keep their old values
+        // phase 5: update in registers, straight-line; invalid steps keep their old values.
+        // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
+        // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
+        float tq[kBrickEdge];
+        if (OW1 && s_rcp && __ballot(!w_small) == 0) {
+            // every lane's weights are small integers: RN(1/wn) from the LDS table + Markstein
+#pragma unroll
+            for (int k = 0; k < kBrickEdge; ++k) {
+                const float wn = ws[k] + 1.0f;
+                const double num = (double)(ws[k] * ts[k]) + dist[k];
+                tq[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kBrickEdge; ++k) {
+                const float wn = OW1 ? ws[k] + 1.0f : (float)((double)ws[k] + fr.ow);
+                const double num = (double)(ws[k] * ts[k]) + (OW1 ? dist[k] : fr.ow * dist[k]);
+                tq[k] = (float)(num / (double)wn);
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kBrickEdge; ++k) {
             const bool ok = (vmask >> k) & 1u;
             const float w_old = ws[k];
-            // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average
-            // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
             const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
-            const float wt = w_old * ts[k];
-            const float tn = (float)(((double)wt + (OW1 ? dist[k] : fr.ow * dist[k])) / (double)wn);
+            const float tn = tq[k];
             // colour (grid_fusion.py:302-314): float32 throughout, round half to even
             float nb, ng, nr;
             if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
@@ -586,47 +637,57 @@ __device__ inline void flush_stats(unsigned long long* s_stat, unsigned long lon
 // Conservative cull of every brick (one lane each) against every frame of the batch, and
 // compaction of the bricks seen by at least one frame into a list of (brick | frame mask << 24):
 // wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
+constexpr int kCullWG = 64 * kMaxBatch;  // k_cull: one wave per frame of the batch
+
+// Brick culling for one batch, hierarchical: one workgroup per superbrick (64 bricks, Vol::sb),
+// one wave per frame.  Wave f tests the superbrick against frame f (wave-uniform) and, if it
+// survives, each lane tests its brick against frame f; the per-brick frame masks meet in LDS and
+// wave 0 appends the kept bricks to the list (one atomicAdd per superbrick with survivors).
+// Every test is at most two cull_brick latencies deep, whatever the batch size.
 template <bool HASH>
-__global__ __launch_bounds__(kWG) void k_cull(Vol v, Batch bt, Table tab, unsigned* list,
-                                             unsigned int* count, unsigned long long* stats) {
-    __shared__ int s_cnt[kWG / 64];
-    __shared__ unsigned int s_base;
+__global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, unsigned* list,
+                                                  unsigned int* count, unsigned long long* stats) {
+    __shared__ unsigned s_mask[64];
     __shared__ unsigned long long s_stat[kNStat];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int f = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid < 64) s_mask[tid] = 0u;
     if (tid < kNStat) s_stat[tid] = 0;
-    const long long nbricks = (long long)v.nb[0] * v.nb[1] * v.nb[2];
-    const long long e = (long long)blockIdx.x * kWG + tid;
-    unsigned fmask = 0;
-    if (e < nbricks) {
-        const int b = (int)e;
-        const int nb12 = v.nb[1] * v.nb[2];
-        const int bx = b / nb12, rem = b - bx * nb12, by = rem / v.nb[2], bz = rem - by * v.nb[2];
-        bool mine = true;
-        if (HASH && v.n_shards > 1) {  // bucket-range ownership
-            const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
-            mine = (int)((home * v.n_shards) / tab.capacity) == v.shard;
-        }
-        if (mine) {
-            const BrickBox box = brick_box(v, bx, by, bz);
-            for (int f = 0; f < bt.n; ++f)
-                if (cull_brick(v, bt.f[f], box)) fmask |= 1u << f;
+    __syncthreads();
+    const int nsy = (v.nb[1] + (1 << v.sb[1]) - 1) >> v.sb[1];
+    const int nsz = (v.nb[2] + (1 << v.sb[2]) - 1) >> v.sb[2];
+    const int si = blockIdx.x;
+    const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
+    const int ex = 1 << v.sb[0], ey = 1 << v.sb[1], ez = 1 << v.sb[2];
+    const int lz = lane & (ez - 1), ly = (lane >> v.sb[2]) & (ey - 1), lx = lane >> (v.sb[1] + v.sb[2]);
+    const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
+    const unsigned e = (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz);
+    if (f < bt.n) {
+        const Frame& fr = bt.f[f];
+        if (cull_brick(v, fr, brick_box(v, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
+            bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
+            if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership
+                const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
+                test = (int)((home * v.n_shards) / tab.capacity) == v.shard;
+            }
+            if (test && cull_brick(v, fr, brick_box(v, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
         }
     }
-    const bool keep = fmask != 0;
-    const unsigned long long m = __ballot(keep);
-    if (lane == 0) s_cnt[wave] = __popcll(m);
     __syncthreads();
-    if (tid == 0) {
-        int tot = 0;
-        for (int w = 0; w < kWG / 64; ++w) tot += s_cnt[w];
-        s_base = tot ? atomicAdd(count, (unsigned)tot) : 0u;
-        s_stat[ST_VISITED] = (unsigned long long)tot;
+    if (tid < 64) {
+        const unsigned fmask = s_mask[lane];
+        const unsigned long long m = __ballot(fmask != 0u);
+        if (m) {
+            unsigned base = 0;
+            if (lane == 0) {
+                base = atomicAdd(count, (unsigned)__popcll(m));
+                s_stat[ST_VISITED] = (unsigned long long)__popcll(m);
+            }
+            base = __shfl(base, 0);
+            if (fmask) list[base + __popcll(m & ((1ull << lane) - 1ull))] = e | (fmask << 24);
+        }
     }
     __syncthreads();
-    int off = 0;
-#pragma unroll
-    for (int w = 0; w < kWG / 64; ++w) off += (w < wave) ? s_cnt[w] : 0;
-    if (keep) list[s_base + off + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)e | (fmask << 24);
     flush_stats(s_stat, stats);
 }
 
@@ -639,13 +700,16 @@ __global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, T
                                                   unsigned long long* stats, const unsigned* list,
                                                   unsigned int* count, int n_list) {
     __shared__ unsigned long long s_stat[kNStat];
+    __shared__ double s_rcp[OW1 ? kRcpTab : 1];  // RN(1/n): weights are small integers when ow == 1
     const int tid = threadIdx.x;
     if (tid < kNStat) s_stat[tid] = 0;
+    if (OW1)
+        for (int i = tid; i < kRcpTab; i += kWG) s_rcp[i] = 1.0 / (double)i;
     __syncthreads();
     const int n = count ? (int)coh_load(count) : n_list;
     const int nw = gridDim.x * (kWG / 64);
     for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
-        integrate_brick<HASH, DK, CK, OW1>(v, bt, pool, tab, list[e], s_stat);
+        integrate_brick<HASH, DK, CK, OW1>(v, bt, pool, tab, list[e], s_stat, OW1 ? s_rcp : nullptr);
     __syncthreads();
     flush_stats(s_stat, stats);
 }

@@ -380,7 +380,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
              int H, int W, const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
-    const unsigned cull_grid = (unsigned)((B.n_bricks + kWG - 1) / kWG);
+    const unsigned cull_grid = B.cull_grid();
     const bool sync = !(flags & TSDF_ASYNC);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
@@ -388,7 +388,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
         TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, nullptr, 1.0, flags, f0, n));
         TSDF_TRY(B.launch_prep(bt, dk, ck, W, H));
-        hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kWG), 0, B.stream, B.vol, bt, h->t, B.list,
+        hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, h->t, B.list,
                            B.count, B.stats);
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;

@@ -86,6 +86,12 @@ struct Base {
     // Workgroups of the integrate kernel: as many as can be resident (occupancy x CUs), capped
     // by the work there can be (4 bricks per workgroup per round).
     unsigned grid_for(const void* kernel);
+    // Workgroups of k_cull: one per superbrick (Vol::sb).
+    unsigned cull_grid() const {
+        long long n = 1;
+        for (int a = 0; a < 3; ++a) n *= (vol.nb[a] + (1 << vol.sb[a]) - 1) >> vol.sb[a];
+        return (unsigned)n;
+    }
     int read_stats(tsdf_stats_t* out, int reset);
     int set_profiling(int on);
     void release();

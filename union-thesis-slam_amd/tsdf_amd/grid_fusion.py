@@ -59,6 +59,26 @@ def encode_color(color_im):
     return _ffi.COLOR_F32, np.ascontiguousarray(folded, dtype=np.float32)
 
 
+def frame_stack(depth, depth_kind, color, color_kind, device_ptrs):
+    """Frame-stack kinds for the batch entry points: default u16 mm / RGB8 for device
+    pointers; for host arrays, taken from (and checked against) the dtypes -- u16|i16 mm or
+    f64 m depth (F,H,W); (F,H,W,3) u8 or folded (F,H,W) f32 colour."""
+    if device_ptrs:
+        return (depth, _ffi.DEPTH_U16_MM if depth_kind is None else depth_kind,
+                color, _ffi.COLOR_RGB8 if color_kind is None else color_kind)
+    depth, color = np.ascontiguousarray(depth), np.ascontiguousarray(color)
+    dk = {np.dtype(np.uint16): _ffi.DEPTH_U16_MM, np.dtype(np.int16): _ffi.DEPTH_U16_MM,
+          np.dtype(np.float64): _ffi.DEPTH_F64_M}.get(depth.dtype)
+    ck = (_ffi.COLOR_RGB8 if color.dtype == np.uint8 and color.ndim == 4 else
+          _ffi.COLOR_F32 if color.dtype == np.float32 and color.ndim == 3 else None)
+    if dk is None or ck is None or depth.ndim != 3 or color.shape[:3] != depth.shape:
+        raise ValueError(f"depth {depth.dtype}{depth.shape} / colour {color.dtype}{color.shape} "
+                         "is not a supported frame stack")
+    if (depth_kind is not None and depth_kind != dk) or (color_kind is not None and color_kind != ck):
+        raise ValueError("depth_kind/color_kind disagree with the array dtypes")
+    return depth, dk, color, ck
+
+
 class TSDFVolume:
     """Volumetric TSDF Fusion of RGB-D Images, on an MI355X.
 
@@ -145,13 +165,15 @@ class TSDFVolume:
         _ffi.call("tsdf_dense_set", self._h, *[_ffi.ptr(x) for x in a])
 
     def integrate_batch(self, depth, color, cam_intr, world_to_cam, obs_weight=None, *,
-                        depth_kind=_ffi.DEPTH_U16_MM, color_kind=_ffi.COLOR_RGB8, hw=None,
-                        device_ptrs=False, sync=True):
+                        depth_kind=None, color_kind=None, hw=None, device_ptrs=False, sync=True):
         """F frames back to back on the volume's stream (the bench's step).
 
         depth/color: host ndarrays (F,H,W[,3]) or, with device_ptrs=True, integer device
         addresses of such arrays already resident in HBM (then hw=(H,W) is required).
-        world_to_cam: (F,4,4) = inv(cam_pose) per frame, computed by the caller."""
+        world_to_cam: (F,4,4) = inv(cam_pose) per frame, computed by the caller.
+        depth_kind/color_kind default to u16 mm / RGB8 for device pointers and are taken from
+        the dtype of host arrays (u16|i16 mm or f64 m; (F,H,W,3) u8 or folded (F,H,W) f32)."""
+        depth, depth_kind, color, color_kind = frame_stack(depth, depth_kind, color, color_kind, device_ptrs)
         T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
         n = T.shape[0]
         H, W = hw if device_ptrs else np.shape(depth)[1:3]

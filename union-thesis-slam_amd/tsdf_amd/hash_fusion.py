@@ -25,7 +25,7 @@ import ctypes
 
 import numpy as np
 
-from . import _ffi
+from . import _ffi, grid_fusion
 from .data_structures import HashEntry, Voxel
 from .grid_fusion import encode_color, encode_depth, volume_geometry
 
@@ -87,8 +87,11 @@ class HashTable:
         _ffi.call("tsdf_hash_integrate", self._h, _ffi.ptr(d), dk, _ffi.ptr(c), ck, im_h, im_w,
                   _ffi.ptr(K), _ffi.ptr(Tinv), 0)
 
-    def integrate_batch(self, depth, color, cam_intr, world_to_cam, *, depth_kind=_ffi.DEPTH_U16_MM,
-                        color_kind=_ffi.COLOR_RGB8, hw=None, device_ptrs=False, sync=True):
+    def integrate_batch(self, depth, color, cam_intr, world_to_cam, *, depth_kind=None,
+                        color_kind=None, hw=None, device_ptrs=False, sync=True):
+        """As TSDFVolume.integrate_batch (obs_weight is never forwarded on the hash path)."""
+        depth, depth_kind, color, color_kind = grid_fusion.frame_stack(depth, depth_kind, color, color_kind,
+                                                                      device_ptrs)
         T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
         H, W = hw if device_ptrs else np.shape(depth)[1:3]
         flags = (_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC)
