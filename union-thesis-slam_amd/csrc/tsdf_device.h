@@ -69,6 +69,10 @@ constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per w
 __device__ inline bool small_int(float w) {
     return w >= 0.0f && w < (float)(kRcpTab - kMaxBatch - 1) && w == truncf(w);
 }
+// a canonical folded colour: an integer B*65536 + G*256 + R in [0, 2^24) (what integrate writes)
+__device__ inline bool canon_color(float c) {
+    return c >= 0.0f && c < 16777216.0f && c == truncf(c);
+}
 struct Batch {
     Frame f[kMaxBatch];
     int n;
@@ -355,6 +359,13 @@ __device__ inline double div_rn(double a, double b, double y) {
     return fma(r, y, q0);
 }
 
+// The same in f32 (y = RN32(1/b)); operands here are integers, so never subnormal.
+__device__ inline float div_rn32(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = fmaf(-q0, b, a);
+    return fmaf(r, y, q0);
+}
+
 __device__ inline double refined_rcp(double z) {
     const double y = __builtin_amdgcn_rcp(z);
     return fma(y, fma(-z, y, 1.0), y);
@@ -412,6 +423,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     bool is_new = false;
     int nupd = 0;
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
+    bool c_canon = true;   // all loaded colours are canonical (canon_color)
 
     for (int fi = 0; fi < bt.n; ++fi) {
         if (!((fmask >> fi) & 1u)) continue;
@@ -516,6 +528,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float4 C = *(const float4*)(pool.color + base);
             ws[0] = W.x; ws[1] = W.y; ws[2] = W.z; ws[3] = W.w;
             w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
+            c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
             ts[0] = T.x; ts[1] = T.y; ts[2] = T.z; ts[3] = T.w;
             cs[0] = C.x; cs[1] = C.y; cs[2] = C.z; cs[3] = C.w;
         }
@@ -525,6 +538,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float4 C = *(const float4*)(pool.color + base + 4);
             ws[4] = W.x; ws[5] = W.y; ws[6] = W.z; ws[7] = W.w;
             w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
+            c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
             ts[4] = T.x; ts[5] = T.y; ts[6] = T.z; ts[7] = T.w;
             cs[4] = C.x; cs[5] = C.y; cs[6] = C.z; cs[7] = C.w;
         }
@@ -540,14 +554,20 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // phase 5: update in registers, straight-line; invalid steps keep their old values.
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
+        // Fast paths (wave-uniform): every lane's weights are small integers -> RN(1/wn) from the
+        // LDS table and Markstein quotients; and, for RGB8 frames, every colour is canonical
+        // (an integer B*65536+G*256+R < 2^24) -> the same for the three colour channels, in f32
+        // with RN32(1/wn) = f32(RN64(1/wn)) (checked for every table entry by the CPU tests).
+        const bool fast_t = OW1 && s_rcp && __ballot(!w_small) == 0;
+        const bool fast_c = CK == 0 && fast_t && __ballot(!c_canon) == 0;
         float tq[kBrickEdge];
-        if (OW1 && s_rcp && __ballot(!w_small) == 0) {
-            // every lane's weights are small integers: RN(1/wn) from the LDS table + Markstein
+        if (fast_t) {
 #pragma unroll
             for (int k = 0; k < kBrickEdge; ++k) {
                 const float wn = ws[k] + 1.0f;
+                const double y = s_rcp[(int)wn];
                 const double num = (double)(ws[k] * ts[k]) + dist[k];
-                tq[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
+                tq[k] = (float)div_rn(num, (double)wn, y);
             }
         } else {
 #pragma unroll
@@ -579,10 +599,19 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float ob = floorf(co / 65536.0f);
             const float og = floorf((co - ob * 65536.0f) / 256.0f);
             const float orr = co - ob * 65536.0f - og * 256.0f;
-            const float cb = fminf(255.0f, rintf((w_old * ob + (OW1 ? nb : fr.ow32 * nb)) / wn));
-            const float cg = fminf(255.0f, rintf((w_old * og + (OW1 ? ng : fr.ow32 * ng)) / wn));
-            const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
-            const float cn = cb * 65536.0f + cg * 256.0f + cr;
+            float cn;
+            if (fast_c) {  // integer channels: the average is <= 255, so min(255, .) is a no-op
+                const float rw = (float)s_rcp[(int)wn];
+                const float cb = rintf(div_rn32(w_old * ob + nb, wn, rw));
+                const float cg = rintf(div_rn32(w_old * og + ng, wn, rw));
+                const float cr = rintf(div_rn32(w_old * orr + nr, wn, rw));
+                cn = cb * 65536.0f + cg * 256.0f + cr;
+            } else {
+                const float cb = fminf(255.0f, rintf((w_old * ob + (OW1 ? nb : fr.ow32 * nb)) / wn));
+                const float cg = fminf(255.0f, rintf((w_old * og + (OW1 ? ng : fr.ow32 * ng)) / wn));
+                const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
+                cn = cb * 65536.0f + cg * 256.0f + cr;
+            }
             ws[k] = ok ? wn : ws[k];
             ts[k] = ok ? tn : ts[k];
             cs[k] = ok ? cn : cs[k];
@@ -696,7 +725,10 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, un
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
 template <bool HASH, int DK, int CK, bool OW1>
-__global__ __launch_bounds__(kWG) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
+#ifndef TSDF_INTEGRATE_ATTR
+#define TSDF_INTEGRATE_ATTR __attribute__((amdgpu_waves_per_eu(4)))  // <= 128 VGPRs: 4 waves/SIMD
+#endif
+__global__ __launch_bounds__(kWG) TSDF_INTEGRATE_ATTR void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
                                                   unsigned long long* stats, const unsigned* list,
                                                   unsigned int* count, int n_list) {
     __shared__ unsigned long long s_stat[kNStat];

@@ -15,7 +15,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtsdf_hip.so")
+LIB_PATH = os.environ.get("TSDF_HIP_LIB") or os.path.join(_HERE, "lib", "libtsdf_hip.so")  # override: A/B builds of the same library
 
 DEPTH_U16_MM, DEPTH_F64_M = 0, 1
 COLOR_RGB8, COLOR_F32 = 0, 1
