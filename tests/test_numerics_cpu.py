@@ -41,3 +41,19 @@ def test_markstein_quotient_matches_ieee_division(tmp_path):
                     "-o", exe, "-lm"], check=True)
     out = subprocess.run([exe], capture_output=True, text=True)
     assert out.returncode == 0 and "mismatches 0" in out.stdout, out.stdout
+
+
+def test_f32_reciprocal_table_is_correctly_rounded():
+    """The colour fast path takes RN32(1/n) as f32(RN64(1/n)) from the kernels' f64 table
+    (n < kRcpTab = 4096); double rounding must not change any entry."""
+    from fractions import Fraction
+    import numpy as np
+    for n in range(1, 4096):
+        y32 = np.float32(np.float64(1.0) / np.float64(n))
+        exact = Fraction(1, n)
+        # y32 is RN32(1/n) iff no other float32 is closer (ties: even mantissa)
+        lo, hi = np.nextafter(y32, np.float32(0)), np.nextafter(y32, np.float32(1))
+        d = abs(Fraction(float(y32)) - exact)
+        assert d <= abs(Fraction(float(lo)) - exact) and d <= abs(Fraction(float(hi)) - exact), n
+        if d == abs(Fraction(float(lo)) - exact) or d == abs(Fraction(float(hi)) - exact):
+            assert int(y32.view(np.uint32)) % 2 == 0, n

@@ -331,10 +331,18 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 // (grid_demo1.py:81-82).  For u16 input the quotient is m * 0.001 with one FMA correction
 // (r = m - 1000 q exactly; q + r * 0.001), which equals RN(m / 1000) for every m in [0, 65535]
 // (checked exhaustively: tools/check_depth_conversion.c).
+// Depth of pixel p in metres = f64(u16) / 1000 (grid_fusion.py via the wrapper's encoding),
+// computed as q = m * 0.001 plus one FMA correction (exact for all 65536 inputs:
+// tools/check_depth_conversion.c).  depth_raw issues the u16 load; depth_m converts.  For f64
+// depth (DK == 1) depth_raw is unused and depth_m loads.
 template <int DK>
-__device__ inline double depth_m(const Frame& fr, int p) {
+__device__ inline unsigned depth_raw(const Frame& fr, int p) {
+    return DK == 0 ? (unsigned)((const unsigned short*)fr.depth)[p] : 0u;
+}
+template <int DK>
+__device__ inline double depth_m(const Frame& fr, int p, unsigned raw) {
     if (DK == 0) {
-        const double m = (double)((const unsigned short*)fr.depth)[p];
+        const double m = (double)raw;
         const double q = m * 0.001;
         return fma(fma(-q, 1000.0, m), 0.001, q);
     }
@@ -364,6 +372,10 @@ __device__ inline float div_rn32(float a, float b, float y) {
     const float q0 = a * y;
     const float r = fmaf(-q0, b, a);
     return fmaf(r, y, q0);
+}
+
+__device__ inline float2 fma2(float2 a, float2 b, float2 c) {  // v_pk_fma_f32
+    return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
 __device__ inline double refined_rcp(double z) {
@@ -468,17 +480,29 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }
         unsigned cand = 0;
         int pix[kBrickEdge];
+        const int W = fr.W, H = fr.H;
 #pragma unroll
         for (int k = 0; k < kBrickEdge; ++k) {
-            const bool c = ((inb >> k) & 1u) && uu[k] >= 0.0 && uu[k] < (double)fr.W &&
-                           vv[k] >= 0.0 && vv[k] < (double)fr.H;
+            const bool c = ((inb >> k) & 1u) && uu[k] >= 0.0 && uu[k] < (double)W &&
+                           vv[k] >= 0.0 && vv[k] < (double)H;
             cand |= (unsigned)c << k;
-            pix[k] = c ? (int)vv[k] * fr.W + (int)uu[k] : 0;
+            // select before converting (branch-free; no out-of-range conversion)
+            pix[k] = (int)(c ? vv[k] : 0.0) * W + (int)(c ? uu[k] : 0.0);
         }
-        // phase 2: gather depth for every step at once (non-candidates read pixel 0, discarded)
+        // phase 2: gather depth and colour for every step at once, before the depth test, so
+        // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
+        // scheduling barrier keeps the compiler from sinking each load next to its use, which
+        // under the 128-VGPR budget it otherwise does, serialising the latencies.
+        unsigned draw[kBrickEdge], cpx[kBrickEdge];
+#pragma unroll
+        for (int k = 0; k < kBrickEdge; ++k) {
+            draw[k] = depth_raw<DK>(fr, pix[k]);
+            cpx[k] = (CK == 0) ? fr.rgbx[pix[k]] : __float_as_uint(((const float*)fr.color)[pix[k]]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         double dep[kBrickEdge];
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) dep[k] = depth_m<DK>(fr, pix[k]);
+        for (int k = 0; k < kBrickEdge; ++k) dep[k] = depth_m<DK>(fr, pix[k], draw[k]);
         // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
         unsigned vmask = 0;
         double dist[kBrickEdge];
@@ -545,12 +569,6 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         loaded |= need;
         dirty |= need;
         touched |= vmask;
-        unsigned cpx[kBrickEdge];
-#pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
-            const int p = ((vmask >> k) & 1u) ? pix[k] : 0;
-            cpx[k] = (CK == 0) ? fr.rgbx[p] : __float_as_uint(((const float*)fr.color)[p]);
-        }
         // phase 5: update in registers, straight-line; invalid steps keep their old values.
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
@@ -595,18 +613,28 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 ng = floorf((nc - nb * 65536.0f) / 256.0f);
                 nr = nc - nb * 65536.0f - ng * 256.0f;
             }
-            const float co = cs[k];
-            const float ob = floorf(co / 65536.0f);
-            const float og = floorf((co - ob * 65536.0f) / 256.0f);
-            const float orr = co - ob * 65536.0f - og * 256.0f;
             float cn;
-            if (fast_c) {  // integer channels: the average is <= 255, so min(255, .) is a no-op
+            if (fast_c) {
+                // canonical colours and integer weights < 4096: decode by bytes, exact integer
+                // numerators by FMA, Markstein quotients (b, g packed); every value is an integer
+                // < 2^24, so each step equals the reference's f32 expression, and the average is
+                // <= 255, so min(255, .) is a no-op
+                const unsigned cu = (unsigned)cs[k];
                 const float rw = (float)s_rcp[(int)wn];
-                const float cb = rintf(div_rn32(w_old * ob + nb, wn, rw));
-                const float cg = rintf(div_rn32(w_old * og + ng, wn, rw));
-                const float cr = rintf(div_rn32(w_old * orr + nr, wn, rw));
-                cn = cb * 65536.0f + cg * 256.0f + cr;
+                const float2 o_bg = make_float2((float)((cu >> 16) & 0xFFu), (float)((cu >> 8) & 0xFFu));
+                const float o_r = (float)(cu & 0xFFu);  // v_cvt_f32_ubyte{0,1,2}
+                const float2 n_bg = make_float2(nb, ng);
+                const float2 w2 = make_float2(w_old, w_old), wn2 = make_float2(wn, wn), r2 = make_float2(rw, rw);
+                const float2 num_bg = fma2(w2, o_bg, n_bg);
+                const float2 q0 = num_bg * r2;
+                const float2 q = fma2(fma2(-q0, wn2, num_bg), r2, q0);
+                const float cr = rintf(div_rn32(fmaf(w_old, o_r, nr), wn, rw));
+                cn = fmaf(rintf(q.x), 65536.0f, fmaf(rintf(q.y), 256.0f, cr));
             } else {
+                const float co = cs[k];
+                const float ob = floorf(co / 65536.0f);
+                const float og = floorf((co - ob * 65536.0f) / 256.0f);
+                const float orr = co - ob * 65536.0f - og * 256.0f;
                 const float cb = fminf(255.0f, rintf((w_old * ob + (OW1 ? nb : fr.ow32 * nb)) / wn));
                 const float cg = fminf(255.0f, rintf((w_old * og + (OW1 ? ng : fr.ow32 * ng)) / wn));
                 const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
