@@ -486,8 +486,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const bool c = ((inb >> k) & 1u) && uu[k] >= 0.0 && uu[k] < (double)W &&
                            vv[k] >= 0.0 && vv[k] < (double)H;
             cand |= (unsigned)c << k;
-            // select before converting (branch-free; no out-of-range conversion)
-            pix[k] = (int)(c ? vv[k] : 0.0) * W + (int)(c ? uu[k] : 0.0);
+            // v*W + u is exact in f64; select before converting (no out-of-range conversion)
+            pix[k] = (int)(c ? fma(vv[k], (double)W, uu[k]) : 0.0);
         }
         // phase 2: gather depth and colour for every step at once, before the depth test, so
         // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
@@ -511,7 +511,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const double diff = dep[k] - zc[k];
             const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
             const double dd = div_rn(diff, v.trunc, v.rtrunc);
-            dist[k] = dd > 1.0 ? 1.0 : dd;  // np.minimum(1, .)
+            dist[k] = fmin(dd, 1.0);  // np.minimum(1, .) (dd is never NaN)
             vmask |= (unsigned)ok << k;
         }
         if (__ballot(vmask != 0) == 0) continue;
