@@ -44,6 +44,8 @@ extern "C" {
 
 #define TSDF_DEVICE_PTRS 1  /* depth/colour pointers are device pointers */
 #define TSDF_ASYNC 2        /* do not synchronise the handle's stream before returning */
+#define TSDF_DEPTH_INVALID_65535 4 /* u16 depth: 65535 mm is invalid (0), the 7-Scenes convention
+                                      of the demos (grid_demo1.py:82: depth_im[depth_im == 65.535] = 0) */
 
 typedef struct tsdf_dense tsdf_dense_t;
 typedef struct tsdf_hash tsdf_hash_t;
@@ -163,6 +165,20 @@ int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf, float* weight, float* color
 int tsdf_hash_sync(tsdf_hash_t* h);
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);
+
+/* ---- frame utilities ---------------------------------------------------------------------
+ * Volume bounds from view frustums: the demo loop grid_demo1.py:50-64 (hash_demo1.py:93-107)
+ * over get_view_frustum (grid_fusion.py:371-383).  For each of
+ * n_frames depth images (H*W each, kind U16_MM or F64_M; host, or device with TSDF_DEVICE_PTRS;
+ * TSDF_DEPTH_INVALID_65535 masks 65535 mm; on HIP device `device`): the image's max depth, the 5 frustum points
+ * transformed by cam_pose (n_frames*16 doubles, camera-to-world, host), then
+ * bounds[2r] = min(bounds[2r], min over points), bounds[2r+1] = max(...) for r = x, y, z
+ * (bounds is in/out: the demo starts from zeros).  Optional outputs: max_depth (n_frames
+ * doubles, metres) and frustum_pts (n_frames x 3 x 5 doubles, get_view_frustum's array).
+ * All values equal the reference's f64 results bit for bit. */
+int tsdf_frustum_bounds(const void* depth, int depth_kind, int n_frames, int height, int width,
+                        const double K[9], const double* cam_poses, int flags, int device,
+                        double* max_depth, double* frustum_pts, double bounds[6]);
 
 /* hash_function over n coordinate triples (host in, host out), computed on the device.  The
  * same arithmetic as the kernels' home-slot computation. */

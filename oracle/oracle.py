@@ -57,6 +57,8 @@ def lib():
         L.oracle_hash_integrate.restype = ctypes.c_int64
         L.oracle_hash_integrate.argtypes = [P, P, ctypes.c_double, ctypes.c_double, P, P, P, P,
                                             P, ctypes.c_int, ctypes.c_int, P, P, P, P]
+        L.oracle_view_frustum.restype = None
+        L.oracle_view_frustum.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, P, P, P]
         L.oracle_hash_keys.restype = None
         L.oracle_hash_keys.argtypes = [P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, P]
         _LIB = L
@@ -230,3 +232,23 @@ def vox_coords_for(dims) -> np.ndarray:
                              indexing="ij")
     return np.concatenate([xv.reshape(1, -1), yv.reshape(1, -1), zv.reshape(1, -1)],
                           axis=0).astype(int).T
+
+
+def view_frustum(max_depth: float, H: int, W: int, K, pose) -> np.ndarray:
+    """grid_fusion.py:371-383 for a frame whose max depth is `max_depth` (metres): (3, 5)."""
+    out = np.zeros((3, 5))
+    K = np.ascontiguousarray(K, dtype=np.float64).reshape(9)
+    pose = np.ascontiguousarray(pose, dtype=np.float64).reshape(16)
+    lib().oracle_view_frustum(float(max_depth), int(H), int(W), _p(K), _p(pose), _p(out))
+    return out
+
+
+def frustum_bounds(max_depths, H, W, K, poses, init=None) -> np.ndarray:
+    """grid_demo1.py:50-64: running min/max of the frustum points, starting from `init`
+    (the demo starts from zeros).  Returns (3, 2)."""
+    b = np.zeros((3, 2)) if init is None else np.array(init, dtype=np.float64)
+    for d, p in zip(max_depths, poses):
+        v = view_frustum(d, H, W, K, p)
+        b[:, 0] = np.minimum(b[:, 0], v.min(axis=1))
+        b[:, 1] = np.maximum(b[:, 1], v.max(axis=1))
+    return b

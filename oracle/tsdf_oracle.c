@@ -222,3 +222,21 @@ void oracle_hash_keys(const int64_t* xyz, int64_t n_pts, int64_t table_size, int
         out[k] = m;
     }
 }
+
+/* get_view_frustum (grid_fusion.py:371-383) of one frame given its max depth, as a (3,5) array:
+ * camera-frame points ((u - cx) * z / fx, (v - cy) * z / fy, z) for u in {0,0,0,W,W}, v in
+ * {0,0,H,0,H}, z in {0,d,d,d,d} (NumPy elementwise order: subtract, multiply, divide), then
+ * rigid_transform (363-368) = np.dot(cam_pose, [p;1]) as OpenBLAS dgemm (the FMA chain above). */
+void oracle_view_frustum(double max_depth, int H, int W, const double* K, const double* pose,
+                         double* out /* 3 x 5, row-major */) {
+    const double us[5] = {0, 0, 0, (double)W, (double)W}, vs_[5] = {0, 0, (double)H, 0, (double)H};
+    for (int j = 0; j < 5; ++j) {
+        const double z = j == 0 ? 0.0 : max_depth;
+        const double x = ((us[j] - K[2]) * z) / K[0];
+        const double y = ((vs_[j] - K[5]) * z) / K[4];
+        for (int r = 0; r < 3; ++r) {
+            const double* t = pose + 4 * r;
+            out[r * 5 + j] = fma(t[3], 1.0, fma(t[2], z, fma(t[1], y, t[0] * x)));
+        }
+    }
+}

@@ -170,3 +170,20 @@ def test_lounge_512_frame0_digest():
               vol._weight_vol_cpu.reshape(-1)[idx], vol._color_vol_cpu.reshape(-1)[idx]):
         h.update(np.ascontiguousarray(a).tobytes())
     assert h.hexdigest() == kat["digest_idx_tsdf_weight_color"]
+
+
+def test_oracle_view_frustum_matches_reference_over_1000_frames():
+    """G6: the oracle's get_view_frustum (grid_fusion.py:371-383, dgemm FMA chain) equals the
+    reference's output bit for bit on all 1000 lounge frames, and the demo's running min/max
+    (grid_demo1.py:50-64) reproduces the bounds the reference's tests hard-code
+    (tests/hash_map_test.py:11, printed to 8 digits)."""
+    g = np.load(os.path.join(GOLD, "frustum_bounds.npz"))
+    H, W = (int(x) for x in g["shape"])
+    md = g["max_depth_mm"] / 1000.0
+    for i in range(0, 1000, 7):
+        v = O.view_frustum(md[i], H, W, g["intr"], g["poses"][i])
+        assert np.array_equal(v.view(np.uint64), g["frustum_pts"][i].view(np.uint64)), i
+    b = O.frustum_bounds(md, H, W, g["intr"], g["poses"])
+    assert np.array_equal(b, g["bounds"])
+    kat = np.array([[-4.22106438, 3.86798203], [-2.6663104, 2.60146141], [0., 5.76272371]])
+    assert np.abs(b - kat).max() < 1e-8

@@ -19,6 +19,9 @@ Fixtures written (data only -- inputs and expected outputs, no reference source)
   golden/synth_c1.npz          two synthetic frames (tsdf_amd.scene) -> 128^3 @ 8 cm room (G2s)
   golden/lounge2cm_kat.json    lounge 2 cm, frames 0-9: per-frame counts + final-state digest (G3)
   golden/lounge512_kat.json    lounge f0 -> 512^3 @ 2 cm: count + digest (G5)
+  golden/frustum_bounds.npz    lounge frames 0-999: per-frame max depth (mm, after the demo's
+                               65535 -> 0 masking), poses, and the reference get_view_frustum
+                               points + the demo's running min/max bounds (G6)
 """
 from __future__ import annotations
 
@@ -240,6 +243,10 @@ def inner():
         with open(os.path.join(GOLD, "lounge2cm_kat.json"), "w") as fh:
             json.dump(kat, fh, indent=1)
 
+    # ---- G6 frustum bounds over the 1000 lounge frames -----------------------------------
+    if want("frustum"):
+        gen_frustum(grid_fusion, cam_intr)
+
     # ---- G5 lounge f0 -> 512^3 @ 2 cm --------------------------------------------------
     if want("lounge512"):
         vol = grid_fusion.TSDFVolume(np.array(C5_BNDS), 0.02, use_gpu=False)
@@ -251,6 +258,39 @@ def inner():
         print("lounge512", kat)
         with open(os.path.join(GOLD, "lounge512_kat.json"), "w") as fh:
             json.dump(kat, fh, indent=1)
+
+
+def gen_frustum(grid_fusion, cam_intr):
+    """G6: grid_demo1.py:50-64 over the 1000 lounge frames.  get_view_frustum only reads the
+    image shape and np.max(depth), so it is called on a zero image of the frame's shape holding
+    the frame's max depth at one pixel -- exactly the reference computation, without shipping
+    1000 depth images."""
+    from PIL import Image
+    n = 1000
+    max_mm = np.zeros(n, np.uint16)
+    poses = np.zeros((n, 4, 4))
+    pts = np.zeros((n, 3, 5))
+    bnds_run = np.zeros((n, 3, 2))
+    vol_bnds = np.zeros((3, 2))
+    for i in range(n):
+        d = np.array(Image.open(os.path.join(REF, "data", "frame-%06d.depth.png" % i)))
+        depth_im = d.astype(float) / 1000.0
+        depth_im[depth_im == 65.535] = 0
+        m = int(np.max(np.where(d == 65535, 0, d)))
+        assert np.max(depth_im) == m / 1000.0
+        max_mm[i] = m
+        poses[i] = np.loadtxt(os.path.join(REF, "data", "frame-%06d.pose.txt" % i))
+        proxy = np.zeros(d.shape)
+        proxy[0, 0] = m / 1000.0
+        vfp = grid_fusion.get_view_frustum(proxy, cam_intr, poses[i])
+        pts[i] = vfp
+        vol_bnds[:, 0] = np.minimum(vol_bnds[:, 0], np.amin(vfp, axis=1))
+        vol_bnds[:, 1] = np.maximum(vol_bnds[:, 1], np.amax(vfp, axis=1))
+        bnds_run[i] = vol_bnds
+    np.savez_compressed(os.path.join(GOLD, "frustum_bounds.npz"), max_depth_mm=max_mm, poses=poses,
+                        intr=cam_intr, shape=np.array(d.shape), frustum_pts=pts, bounds_running=bnds_run,
+                        bounds=vol_bnds)
+    print("frustum bounds", vol_bnds.tolist())
 
 
 def main():

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("TSDF_HIP_LIB") or os.path.join(_HERE, "lib", "libtsdf
 
 DEPTH_U16_MM, DEPTH_F64_M = 0, 1
 COLOR_RGB8, COLOR_F32 = 0, 1
-DEVICE_PTRS, ASYNC = 1, 2
+DEVICE_PTRS, ASYNC, DEPTH_INVALID_65535 = 1, 2, 4
 
 E_ARG, E_HIP, E_NODEV, E_CAPACITY, E_OOM = -1, -2, -3, -4, -5
 
@@ -68,6 +68,7 @@ SIGNATURES = {
     "tsdf_device_count": [_P],
     "tsdf_dense_create": [_P, _P, _P, _D, _D, _I, _P],
     "tsdf_dense_create_shard": [_P, _I, _I, _P, _D, _D, _I, _P],
+    "tsdf_frustum_bounds": [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P],
     "tsdf_dense_destroy": [_P],
     "tsdf_dense_reset": [_P],
     "tsdf_dense_integrate": [_P, _P, _I, _P, _I, _I, _I, _P, _P, _D, _I],

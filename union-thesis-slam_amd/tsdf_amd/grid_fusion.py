@@ -233,3 +233,49 @@ def get_view_frustum(depth_im, cam_intr, cam_pose):
     cam = np.stack([(u - cam_intr[0, 2]) * z / cam_intr[0, 0],
                     (v - cam_intr[1, 2]) * z / cam_intr[1, 1], z], axis=1)
     return rigid_transform(cam, cam_pose).T
+
+
+def view_frustum_bounds(depth_frames, cam_intr, cam_poses, init=None, *, invalid_65535=False,
+                        device=0, device_ptrs=False, hw=None, depth_kind=None, n_frames=None,
+                        return_max_depth=False, return_points=False):
+    """Volume bounds from the union of the frames' view frustums, on the GPU: the demo loop
+    grid_demo1.py:50-64 (hash_demo1.py:93-107) over get_view_frustum (grid_fusion.py:371-383).
+
+    depth_frames: (F,H,W) u16 millimetres or f64 metres (host), or with device_ptrs=True a device
+    address of F such frames (then hw=(H,W), n_frames=F and depth_kind are required).
+    cam_poses: (F,4,4) camera-to-world.  init: starting (3,2) bounds; the demo starts from zeros.
+    invalid_65535: u16 65535 mm counts as 0 (the demos' `depth_im[depth_im == 65.535] = 0`).
+    Returns the (3,2) bounds [, per-frame max depth (F,)] [, frustum points (F,3,5)]."""
+    poses = np.ascontiguousarray(np.asarray(cam_poses, dtype=np.float64).reshape(-1, 16))
+    F = poses.shape[0]
+    if device_ptrs:
+        if hw is None or depth_kind is None or n_frames is None:
+            raise ValueError("device_ptrs needs hw, depth_kind and n_frames")
+        H, W = hw
+        dk, d = depth_kind, depth_frames
+        if n_frames != F:
+            raise ValueError("n_frames differs from the number of poses")
+    else:
+        d = np.ascontiguousarray(depth_frames)
+        if d.ndim != 3 or d.shape[0] != F:
+            raise ValueError(f"depth_frames {d.shape} does not match {F} poses")
+        dk = {np.dtype(np.uint16): _ffi.DEPTH_U16_MM, np.dtype(np.int16): _ffi.DEPTH_U16_MM,
+              np.dtype(np.float64): _ffi.DEPTH_F64_M}.get(d.dtype)
+        if dk is None:
+            raise ValueError(f"depth dtype {d.dtype}: use uint16 millimetres or float64 metres")
+        if depth_kind is not None and depth_kind != dk:
+            raise ValueError("depth_kind disagrees with the array dtype")
+        H, W = d.shape[1:]
+    b = np.zeros((3, 2)) if init is None else np.array(init, dtype=np.float64).reshape(3, 2)
+    b = np.ascontiguousarray(b)
+    md = np.empty(F) if return_max_depth else None
+    pts = np.empty((F, 3, 5)) if return_points else None
+    flags = (_ffi.DEVICE_PTRS if device_ptrs else 0) | (_ffi.DEPTH_INVALID_65535 if invalid_65535 else 0)
+    _ffi.call("tsdf_frustum_bounds", _ffi.ptr(d), dk, F, int(H), int(W), _ffi.ptr(_ffi.f64(cam_intr, 9)),
+              _ffi.ptr(poses), flags, int(device), _ffi.ptr(md), _ffi.ptr(pts), _ffi.ptr(b))
+    out = [b]
+    if return_max_depth:
+        out.append(md)
+    if return_points:
+        out.append(pts)
+    return out[0] if len(out) == 1 else tuple(out)
