@@ -255,3 +255,58 @@ def test_long_batch_without_host_sync_matches_oracle(gf):
     T, W, C = vol.get_state()
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
     assert vol.stats()["voxel_updates"] == n
+
+
+def test_host_ingest_double_buffered_equals_device_path(gf):
+    """Frame ingest: 21 host frames (3 batches, both staging slots, one
+    reused) from pageable numpy arrays and from a pinned torch tensor equal the device-resident
+    run bit for bit; the call returns with the host arrays no longer needed."""
+    import torch
+    d, c, poses = _synth(21, start=5)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    bnds = np.array([[0.0, 10.24]] * 3)
+    Tinv = np.linalg.inv(poses)
+    host = gf.TSDFVolume(bnds.copy(), 0.08)
+    pinned = gf.TSDFVolume(bnds.copy(), 0.08)
+    dev = gf.TSDFVolume(bnds.copy(), 0.08)
+    dh, ch = np.ascontiguousarray(d).copy(), np.ascontiguousarray(c).copy()
+    host.integrate_batch(dh, ch, K, Tinv, sync=False)
+    dh[:] = 0  # the caller may reuse its buffers as soon as the call returns
+    ch[:] = 0
+    dp = torch.from_numpy(np.ascontiguousarray(d)).pin_memory()
+    cp = torch.from_numpy(np.ascontiguousarray(c)).pin_memory()
+    pinned.integrate_batch(dp.data_ptr(), cp.data_ptr(), K, Tinv, hw=d.shape[1:], sync=True)
+    dd, cc = torch.from_numpy(np.ascontiguousarray(d)).cuda(), torch.from_numpy(np.ascontiguousarray(c)).cuda()
+    torch.cuda.synchronize()
+    dev.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True)
+    host.sync()
+    A, B, C = host.get_state(), pinned.get_state(), dev.get_state()
+    for a, b, e in zip(A, B, C):
+        assert _same(a, e) and _same(b, e)
+    assert host.stats()["voxel_updates"] == dev.stats()["voxel_updates"] > 0
+
+
+def test_invalid_65535_mask_on_device(gf):
+    """Raw u16 frames with 65535 pixels + invalid_65535 equal the demos' host masking
+    (depth_im[depth_im == 65.535] = 0, grid_demo1.py:82) fed through the oracle."""
+    K = lounge_intrinsics()
+    bnds = np.array(C1)
+    frames = [load_lounge(i) for i in range(3)]
+    raw = np.stack([f[0] for f in frames]).astype(np.uint16)
+    raw[:, 100:140, 200:260] = 65535
+    raw[1, 300:310, :] = 65535
+    rgb = np.stack([f[2] for f in frames])
+    poses = np.stack([f[3] for f in frames])
+    vol = gf.TSDFVolume(bnds.copy(), 0.04)
+    vol.integrate_batch(raw, rgb, K, np.linalg.inv(poses), invalid_65535=True)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.04)
+    for i in range(3):
+        m = raw[i].astype(float) / 1000.0
+        m[m == 65.535] = 0
+        orc.integrate(rgb[i], m, K, poses[i])
+    T, W, Cc = vol.get_state()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(Cc, orc._color_vol_cpu)
+    # without the mask 65.535 m is a valid (far) depth: a different volume
+    vol2 = gf.TSDFVolume(bnds.copy(), 0.04)
+    vol2.integrate_batch(raw, rgb, K, np.linalg.inv(poses))
+    assert not _same(vol2.get_state()[1], W)

@@ -118,6 +118,12 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];
     if (n_bricks >= (1ll << 24)) return set_error(TSDF_E_ARG, "too many bricks (%lld >= 2^24)", n_bricks);
     TSDF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    TSDF_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+        TSDF_HIP(hipEventCreateWithFlags(&ev_copied[k], hipEventDisableTiming));
+        TSDF_HIP(hipEventCreateWithFlags(&ev_free[k], hipEventDisableTiming));
+        TSDF_HIP(hipEventRecord(ev_free[k], stream));  // both slots start free
+    }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
     TSDF_HIP(hipMalloc(&list, sizeof(unsigned) * (size_t)n_bricks));
     TSDF_HIP(hipMalloc(&count, sizeof(unsigned int) * 4));
@@ -186,23 +192,39 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
     const size_t cbytes = npx * (ck == TSDF_COLOR_RGB8 ? 3 : 4);
     const char* d = (const char*)depth + dbytes * (size_t)first;
     const char* c = (const char*)color + cbytes * (size_t)first;
-    if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames (pageable host memory)
-        if (st_depth_bytes < dbytes * kMaxBatch) {
+    if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames into slot call_batch & 1
+        const int slot = (int)(call_batch & 1);
+        if (st_depth_bytes < dbytes * kMaxBatch || st_color_bytes < cbytes * kMaxBatch) {
             TSDF_HIP(hipStreamSynchronize(stream));
-            if (st_depth) TSDF_HIP(hipFree(st_depth));
-            TSDF_HIP(hipMalloc(&st_depth, dbytes * kMaxBatch));
+            TSDF_HIP(hipStreamSynchronize(cstream));
+            for (int k = 0; k < 2; ++k) {
+                if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
+                if (st_color[k]) TSDF_HIP(hipFree(st_color[k]));
+                st_depth[k] = st_color[k] = nullptr;
+            }
+            st_depth_bytes = st_color_bytes = 0;
+            for (int k = 0; k < 2; ++k) {
+                TSDF_HIP(hipMalloc(&st_depth[k], dbytes * kMaxBatch));
+                TSDF_HIP(hipMalloc(&st_color[k], cbytes * kMaxBatch));
+            }
             st_depth_bytes = dbytes * kMaxBatch;
-        }
-        if (st_color_bytes < cbytes * kMaxBatch) {
-            TSDF_HIP(hipStreamSynchronize(stream));
-            if (st_color) TSDF_HIP(hipFree(st_color));
-            TSDF_HIP(hipMalloc(&st_color, cbytes * kMaxBatch));
             st_color_bytes = cbytes * kMaxBatch;
         }
-        TSDF_HIP(hipMemcpyAsync(st_depth, d, dbytes * n, hipMemcpyHostToDevice, stream));
-        TSDF_HIP(hipMemcpyAsync(st_color, c, cbytes * n, hipMemcpyHostToDevice, stream));
-        d = (const char*)st_depth;
-        c = (const char*)st_color;
+        TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[slot], 0));
+        TSDF_HIP(hipMemcpyAsync(st_depth[slot], d, dbytes * n, hipMemcpyHostToDevice, cstream));
+        TSDF_HIP(hipMemcpyAsync(st_color[slot], c, cbytes * n, hipMemcpyHostToDevice, cstream));
+        TSDF_HIP(hipEventRecord(ev_copied[slot], cstream));
+        TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
+        d = (const char*)st_depth[slot];
+        c = (const char*)st_color[slot];
+    }
+    const bool mask = (flags & TSDF_DEPTH_INVALID_65535) && dk == TSDF_DEPTH_U16_MM;
+    if (mask && dmask_px < npx) {
+        TSDF_HIP(hipStreamSynchronize(stream));
+        if (dmask) TSDF_HIP(hipFree(dmask));
+        dmask = nullptr;
+        TSDF_HIP(hipMalloc(&dmask, sizeof(unsigned short) * npx * kMaxBatch));
+        dmask_px = npx;
     }
     bt->n = n;
     for (int i = 0; i < n; ++i) {
@@ -217,7 +239,9 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->ow32 = (float)fr->ow;
         fr->H = H;
         fr->W = W;
-        fr->depth = d + dbytes * i;
+        fr->depth_src = d + dbytes * i;
+        fr->depth_mask = mask ? dmask + npx * i : nullptr;
+        fr->depth = mask ? (const void*)fr->depth_mask : fr->depth_src;
         fr->color = c + cbytes * i;
         fr->rgbx = rgbx + npx * i;
         fr->pyr = pyr + (size_t)lay.total * i;
@@ -229,6 +253,42 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
             fr->pyr_h[L] = lay.h[L];
         }
     }
+    return TSDF_OK;
+}
+
+// Page-lock [p, p + bytes) for the call unless it is already device-visible host memory.
+static int pin_range(std::vector<const void*>& pinned, const void* p, size_t bytes) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type != hipMemoryTypeUnregistered)
+        return TSDF_OK;  // pinned, registered or device memory already
+    (void)hipGetLastError();
+    const hipError_t e = hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault);
+    if (e == hipSuccess) pinned.push_back(p);
+    else (void)hipGetLastError();  // not registrable: hipMemcpyAsync still copies (staged)
+    return TSDF_OK;
+}
+
+int Base::begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags) {
+    call_batch = 0;
+    if (flags & TSDF_DEVICE_PTRS) return TSDF_OK;
+    TSDF_TRY(pin_range(pinned, depth, dbytes));
+    if (color != depth) TSDF_TRY(pin_range(pinned, color, cbytes));
+    return TSDF_OK;
+}
+
+int Base::end_batch(int flags) {
+    if (!(flags & TSDF_DEVICE_PTRS)) TSDF_HIP(hipEventRecord(ev_free[call_batch & 1], stream));
+    ++call_batch;
+    return TSDF_OK;
+}
+
+int Base::end_call(int flags) {
+    if (flags & TSDF_DEVICE_PTRS) return TSDF_OK;
+    // the caller's host arrays are borrowed for the call: every copy has landed before return
+    const hipError_t e = hipStreamSynchronize(cstream);
+    for (const void* p : pinned) (void)hipHostUnregister(const_cast<void*>(p));
+    pinned.clear();
+    TSDF_HIP(e);
     return TSDF_OK;
 }
 
@@ -307,15 +367,27 @@ void Base::release() {
     if (list) (void)hipFree(list);
     if (count) (void)hipFree(count);
     if (stats) (void)hipFree(stats);
-    if (st_depth) (void)hipFree(st_depth);
-    if (st_color) (void)hipFree(st_color);
+    if (cstream) (void)hipStreamSynchronize(cstream);
+    for (int k = 0; k < 2; ++k) {
+        if (st_depth[k]) (void)hipFree(st_depth[k]);
+        if (st_color[k]) (void)hipFree(st_color[k]);
+        if (ev_copied[k]) (void)hipEventDestroy(ev_copied[k]);
+        if (ev_free[k]) (void)hipEventDestroy(ev_free[k]);
+        st_depth[k] = st_color[k] = nullptr;
+        ev_copied[k] = ev_free[k] = nullptr;
+    }
+    if (dmask) (void)hipFree(dmask);
+    dmask = nullptr;
+    for (const void* p : pinned) (void)hipHostUnregister(const_cast<void*>(p));
+    pinned.clear();
+    if (cstream) (void)hipStreamDestroy(cstream);
+    cstream = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     pyr = nullptr;
     rgbx = nullptr;
     list = nullptr;
     count = nullptr;
     stats = nullptr;
-    st_depth = st_color = nullptr;
     stream = nullptr;
 }
 

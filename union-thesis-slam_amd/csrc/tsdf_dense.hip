@@ -46,6 +46,9 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     const Table no_table{};
     const unsigned cull_grid = B.cull_grid();
     const unsigned grid = B.grid_for((const void*)k_integrate<false, 0, 0, false>);
+    TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
+                          frame_bytes_color(ck, H, W) * n_frames, flags));
+    CallGuard guard(B, flags);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
@@ -78,8 +81,10 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
         }
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
+        TSDF_TRY(B.end_batch(flags));
         B.frames += n;
     }
+    TSDF_TRY(guard.finish());
     if (!(flags & TSDF_ASYNC)) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;
 }

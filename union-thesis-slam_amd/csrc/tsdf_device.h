@@ -49,7 +49,9 @@ struct Frame {
     double ow;                // obs_weight as a Python float (f64)
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
-    const void* depth;        // the caller's depth: u16 millimetres or f64 metres
+    const void* depth;        // depth read by cull/integrate: u16 millimetres or f64 metres
+    const void* depth_src;    // depth read by k_prep (== depth unless masking)
+    unsigned short* depth_mask;  // TSDF_DEPTH_INVALID_65535: k_prep writes the masked u16 here
     const void* color;        // the caller's colour (RGB8 or folded f32)
     const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
@@ -810,8 +812,17 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
             const int x = x0 + dx, y = y0 + dy;
             if (x < fr.W && y < fr.H) {
                 const int p = y * fr.W + x;
-                const float d = DK == 0 ? (float)((const unsigned short*)fr.depth)[p] * 1e-3f
-                                        : (float)((const double*)fr.depth)[p];
+                float d;
+                if (DK == 0) {
+                    unsigned v = ((const unsigned short*)fr.depth_src)[p];
+                    if (fr.depth_mask) {  // the demos' depth_im[depth_im == 65.535] = 0
+                        v = (v == 65535u) ? 0u : v;
+                        fr.depth_mask[p] = (unsigned short)v;
+                    }
+                    d = (float)v * 1e-3f;
+                } else {
+                    d = (float)((const double*)fr.depth_src)[p];
+                }
                 if (CK == 0) {
                     const unsigned char* q = (const unsigned char*)fr.color + 3 * (size_t)p;
                     rgbx[p] = (unsigned)q[0] | ((unsigned)q[1] << 8) | ((unsigned)q[2] << 16);

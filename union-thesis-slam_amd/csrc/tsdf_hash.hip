@@ -382,6 +382,9 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_HIP(hipSetDevice(B.device));
     const unsigned cull_grid = B.cull_grid();
     const bool sync = !(flags & TSDF_ASYNC);
+    TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
+                          frame_bytes_color(ck, H, W) * n_frames, flags));
+    CallGuard guard(B, flags);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
@@ -399,7 +402,10 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
         TSDF_HIP(hipGetLastError());
         B.frames += n;
-        if (!sync) continue;
+        if (!sync) {
+            TSDF_TRY(B.end_batch(flags));
+            continue;
+        }
         // Synchronous: recover from a full table/pool exactly (the skipped bricks were not
         // touched by any frame of the batch), then keep the reference's load-factor policy.
         TSDF_TRY(read_state(h));
@@ -425,8 +431,10 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
             TSDF_TRY(read_state(h));
         }
         if (h->host_st.n_overflow > 0) return set_error(TSDF_E_CAPACITY, "could not make room in the hash table");
+        TSDF_TRY(B.end_batch(flags));  // the overflow re-runs above read this batch's frames
         TSDF_TRY(ensure_room(h));
     }
+    TSDF_TRY(guard.finish());
     if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;
 }

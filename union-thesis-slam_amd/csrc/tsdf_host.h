@@ -68,11 +68,20 @@ struct Base {
     unsigned long long* stats = nullptr;  // kNStat x kStatSpread
     long long frames = 0;
     Profiler prof;
-    // staging for host-pointer frames
-    void* st_depth = nullptr;
-    size_t st_depth_bytes = 0;
-    void* st_color = nullptr;
-    size_t st_color_bytes = 0;
+    // Host-pointer frames (frame ingest): two device staging slots filled
+    // by DMA on a copy stream while the compute stream integrates the other slot's batch.
+    // The caller's host arrays are page-locked for the call (hipHostRegister) when they are
+    // not already, so the copies are true asynchronous DMA.
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_copied[2] = {nullptr, nullptr};  // slot's frames landed (copy stream)
+    hipEvent_t ev_free[2] = {nullptr, nullptr};    // slot's last reader finished (compute stream)
+    void* st_depth[2] = {nullptr, nullptr};
+    void* st_color[2] = {nullptr, nullptr};
+    size_t st_depth_bytes = 0, st_color_bytes = 0;
+    unsigned short* dmask = nullptr;  // kMaxBatch masked u16 depth images (TSDF_DEPTH_INVALID_65535)
+    size_t dmask_px = 0;
+    long long call_batch = 0;         // batches issued in the current call
+    std::vector<const void*> pinned;  // ranges this call registered (unregistered by end_call)
 
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
@@ -82,6 +91,12 @@ struct Base {
     int prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
                       int W, const double K[9], const double* Tinv, const double* ow,
                       double ow_default, int flags, int first, int n);
+    // Around the batches of one integrate call: begin_call pins the caller's host arrays (if
+    // host pointers), end_batch marks the batch's staging slot reusable once the compute stream
+    // has finished with it, end_call waits for the copies and unpins.
+    int begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags);
+    int end_batch(int flags);
+    int end_call(int flags);
     int launch_prep(const Batch& bt, int dk, int ck, int W, int H);
     // Workgroups of the integrate kernel: as many as can be resident (occupancy x CUs), capped
     // by the work there can be (4 bricks per workgroup per round).
@@ -96,6 +111,24 @@ struct Base {
     int set_profiling(int on);
     void release();
 };
+
+// end_call on every exit path of an integrate call (error returns included).
+struct CallGuard {
+    Base& b;
+    int flags;
+    bool done = false;
+    CallGuard(Base& b_, int f) : b(b_), flags(f) {}
+    int finish() {
+        done = true;
+        return b.end_call(flags);
+    }
+    ~CallGuard() {
+        if (!done) (void)b.end_call(flags);
+    }
+};
+
+inline size_t frame_bytes_depth(int dk, int H, int W) { return (size_t)H * W * (dk == TSDF_DEPTH_U16_MM ? 2 : 8); }
+inline size_t frame_bytes_color(int ck, int H, int W) { return (size_t)H * W * (ck == TSDF_COLOR_RGB8 ? 3 : 4); }
 
 int check_frame_args(const void* depth, int dk, const void* color, int ck, int H, int W,
                      const double* K, const double* Tinv);

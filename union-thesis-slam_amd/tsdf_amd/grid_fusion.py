@@ -63,7 +63,7 @@ def frame_stack(depth, depth_kind, color, color_kind, device_ptrs):
     """Frame-stack kinds for the batch entry points: default u16 mm / RGB8 for device
     pointers; for host arrays, taken from (and checked against) the dtypes -- u16|i16 mm or
     f64 m depth (F,H,W); (F,H,W,3) u8 or folded (F,H,W) f32 colour."""
-    if device_ptrs:
+    if device_ptrs or isinstance(depth, int):  # raw addresses (device, or pinned host)
         return (depth, _ffi.DEPTH_U16_MM if depth_kind is None else depth_kind,
                 color, _ffi.COLOR_RGB8 if color_kind is None else color_kind)
     depth, color = np.ascontiguousarray(depth), np.ascontiguousarray(color)
@@ -165,20 +165,25 @@ class TSDFVolume:
         _ffi.call("tsdf_dense_set", self._h, *[_ffi.ptr(x) for x in a])
 
     def integrate_batch(self, depth, color, cam_intr, world_to_cam, obs_weight=None, *,
-                        depth_kind=None, color_kind=None, hw=None, device_ptrs=False, sync=True):
+                        depth_kind=None, color_kind=None, hw=None, device_ptrs=False, sync=True,
+                        invalid_65535=False):
         """F frames back to back on the volume's stream (the bench's step).
 
         depth/color: host ndarrays (F,H,W[,3]) or, with device_ptrs=True, integer device
         addresses of such arrays already resident in HBM (then hw=(H,W) is required).
         world_to_cam: (F,4,4) = inv(cam_pose) per frame, computed by the caller.
         depth_kind/color_kind default to u16 mm / RGB8 for device pointers and are taken from
-        the dtype of host arrays (u16|i16 mm or f64 m; (F,H,W,3) u8 or folded (F,H,W) f32)."""
+        the dtype of host arrays (u16|i16 mm or f64 m; (F,H,W,3) u8 or folded (F,H,W) f32).
+        Host arrays are page-locked for the call and copied by DMA into two alternating device
+        slots while the previous batch integrates.  invalid_65535: u16 65535 mm is invalid (0),
+        the demos' `depth_im[depth_im == 65.535] = 0` (grid_demo1.py:82) done on the device."""
         depth, depth_kind, color, color_kind = frame_stack(depth, depth_kind, color, color_kind, device_ptrs)
         T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
         n = T.shape[0]
-        H, W = hw if device_ptrs else np.shape(depth)[1:3]
+        H, W = hw if (device_ptrs or isinstance(depth, int)) else np.shape(depth)[1:3]
         ow = None if obs_weight is None else _ffi.f64(obs_weight, n)
-        flags = (_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC)
+        flags = ((_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC) |
+                 (_ffi.DEPTH_INVALID_65535 if invalid_65535 else 0))
         _ffi.call("tsdf_dense_integrate_batch", self._h, n, _ffi.ptr(depth), depth_kind,
                   _ffi.ptr(color), color_kind, int(H), int(W), _ffi.ptr(_ffi.f64(cam_intr, 9)),
                   _ffi.ptr(T), _ffi.ptr(ow), flags)

@@ -88,13 +88,14 @@ class HashTable:
                   _ffi.ptr(K), _ffi.ptr(Tinv), 0)
 
     def integrate_batch(self, depth, color, cam_intr, world_to_cam, *, depth_kind=None,
-                        color_kind=None, hw=None, device_ptrs=False, sync=True):
+                        color_kind=None, hw=None, device_ptrs=False, sync=True, invalid_65535=False):
         """As TSDFVolume.integrate_batch (obs_weight is never forwarded on the hash path)."""
         depth, depth_kind, color, color_kind = grid_fusion.frame_stack(depth, depth_kind, color, color_kind,
                                                                       device_ptrs)
         T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
-        H, W = hw if device_ptrs else np.shape(depth)[1:3]
-        flags = (_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC)
+        H, W = hw if (device_ptrs or isinstance(depth, int)) else np.shape(depth)[1:3]
+        flags = ((_ffi.DEVICE_PTRS if device_ptrs else 0) | (0 if sync else _ffi.ASYNC) |
+                 (_ffi.DEPTH_INVALID_65535 if invalid_65535 else 0))
         _ffi.call("tsdf_hash_integrate_batch", self._h, T.shape[0], _ffi.ptr(depth), depth_kind,
                   _ffi.ptr(color), color_kind, int(H), int(W), _ffi.ptr(_ffi.f64(cam_intr, 9)),
                   _ffi.ptr(T), flags)
