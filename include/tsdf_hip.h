@@ -64,6 +64,8 @@ typedef struct {
     int64_t kernel_launches;  /* integrate-kernel launches timed */
     int64_t bricks_skipped;   /* hash: bricks skipped for lack of table/pool space (must be 0
                                  after a synchronous call; see tsdf_hash_integrate_batch) */
+    int64_t list_errors;      /* brick-list entries out of range, dropped by the integrate kernel
+                                 (always 0 unless device memory was corrupted) */
 } tsdf_stats_t;
 
 typedef struct {

@@ -111,6 +111,7 @@ def test_empty_and_invalid_depth_is_a_no_op(gf):
     away[:3, 0] *= -1
     vol.integrate(rgb, depth, K, away)
     T, W, C = vol.get_state()
+    assert vol.stats()["list_errors"] == 0
     orc = O.OracleTSDFVolume(np.array(C1), 0.04)
     orc.integrate(rgb, depth, K, away)
     assert int(W.sum()) == int(orc._weight_vol_cpu.sum())
@@ -255,6 +256,7 @@ def test_long_batch_without_host_sync_matches_oracle(gf):
     T, W, C = vol.get_state()
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
     assert vol.stats()["voxel_updates"] == n
+    assert vol.stats()["list_errors"] == 0
 
 
 def test_host_ingest_double_buffered_equals_device_path(gf):

@@ -1,6 +1,7 @@
 // tsdf_dense.hip -- dense TSDF grid: the MI355X replacement of TSDFVolume
 // (grid_fusion.py:19-320).  HBM layout: three f32 SoA arrays of 512-voxel bricks, brick b =
 // (bx*nby + by)*nbz + bz, brick-local voxel (x*8 + y)*8 + z.
+#include <cstdlib>
 #include <cstring>
 
 #include "tsdf_host.h"
@@ -9,6 +10,7 @@ using namespace tsdf;
 
 struct tsdf_dense {
     Base b;
+    int nz = 4;  // z-steps per wave in k_integrate (8: a brick per wave; 4: a z-half per wave)
 };
 
 namespace {
@@ -45,7 +47,8 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     TSDF_HIP(hipSetDevice(B.device));
     const Table no_table{};
     const unsigned cull_grid = B.cull_grid();
-    const unsigned grid = B.grid_for((const void*)k_integrate<false, 0, 0, false>);
+    const unsigned grid = h->nz == 4 ? 2 * B.grid_for((const void*)k_integrate<false, 0, 0, true, 4>)
+                                     : B.grid_for((const void*)k_integrate<false, 0, 0, true, 8>);
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
@@ -62,21 +65,30 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
         bool ow1 = true;
         for (int i = 0; i < n; ++i) ow1 = ow1 && bt.f[i].ow == 1.0;
         const unsigned* L = (const unsigned*)B.list;
-        const int sel = (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (ck == TSDF_COLOR_RGB8 ? 0 : 2) | (ow1 ? 1 : 0);
+        const int sel = (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (ck == TSDF_COLOR_RGB8 ? 0 : 2) | (ow1 ? 1 : 0) |
+                        (h->nz == 4 ? 8 : 0);
         switch (sel) {
-#define TSDF_LAUNCH(S, DK_, CK_, OW_)                                                                  \
+#define TSDF_LAUNCH(S, DK_, CK_, OW_, NZ_)                                                             \
     case S:                                                                                            \
-        hipLaunchKernelGGL((k_integrate<false, DK_, CK_, OW_>), dim3(grid), dim3(kWG), 0, B.stream, B.vol, bt, \
-                           B.pool, no_table, B.stats, L, B.count, 0);                                  \
+        hipLaunchKernelGGL((k_integrate<false, DK_, CK_, OW_, NZ_>), dim3(grid), dim3(kWG), 0, B.stream,   \
+                           B.vol, bt, B.pool, no_table, B.stats, L, B.count, 0);                       \
         break;
-            TSDF_LAUNCH(0, 0, 0, false)
-            TSDF_LAUNCH(1, 0, 0, true)
-            TSDF_LAUNCH(2, 0, 1, false)
-            TSDF_LAUNCH(3, 0, 1, true)
-            TSDF_LAUNCH(4, 1, 0, false)
-            TSDF_LAUNCH(5, 1, 0, true)
-            TSDF_LAUNCH(6, 1, 1, false)
-            TSDF_LAUNCH(7, 1, 1, true)
+            TSDF_LAUNCH(0, 0, 0, false, 8)
+            TSDF_LAUNCH(1, 0, 0, true, 8)
+            TSDF_LAUNCH(2, 0, 1, false, 8)
+            TSDF_LAUNCH(3, 0, 1, true, 8)
+            TSDF_LAUNCH(4, 1, 0, false, 8)
+            TSDF_LAUNCH(5, 1, 0, true, 8)
+            TSDF_LAUNCH(6, 1, 1, false, 8)
+            TSDF_LAUNCH(7, 1, 1, true, 8)
+            TSDF_LAUNCH(8, 0, 0, false, 4)
+            TSDF_LAUNCH(9, 0, 0, true, 4)
+            TSDF_LAUNCH(10, 0, 1, false, 4)
+            TSDF_LAUNCH(11, 0, 1, true, 4)
+            TSDF_LAUNCH(12, 1, 0, false, 4)
+            TSDF_LAUNCH(13, 1, 0, true, 4)
+            TSDF_LAUNCH(14, 1, 1, false, 4)
+            TSDF_LAUNCH(15, 1, 1, true, 4)
 #undef TSDF_LAUNCH
         }
         TSDF_HIP(hipGetLastError());
@@ -130,6 +142,7 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
     int r = h->b.init(device, dims, index_offset, origin, voxel_size, trunc);
     if (r == TSDF_OK) {
         h->b.vol.xstride = xstride;
+        if (const char* e = getenv("TSDF_DENSE_NZ")) h->nz = atoi(e) == 8 ? 8 : 4;  // A/B override
         if (xstride > kBrickEdge) {  // cyclic shard: superbricks one column wide, 8x8 in y, z
             h->b.vol.sb[0] = 0;
             h->b.vol.sb[1] = h->b.vol.sb[2] = 3;

@@ -26,7 +26,7 @@ constexpr unsigned long long kEmpty = ~0ull;
 constexpr unsigned long long kTomb = ~0ull - 1ull;
 
 enum Stat { ST_VOXELS = 0, ST_VISITED, ST_TOUCHED, ST_ALLOC, ST_PROBE, ST_LOOKUPS, ST_OVERFLOW,
-            ST_PROBE_MAX, kNStat };
+            ST_PROBE_MAX, ST_BAD_ENTRY, kNStat };
 
 // Volume geometry (by value in kernel arguments -> scalar registers).
 struct Vol {
@@ -402,14 +402,29 @@ __device__ inline double readlane_f64(double x, int l) {
 // go through the phases together (project -> gather depth -> test -> colour -> update) to keep
 // many loads in flight per lane.
 // ---------------------------------------------------------------------------------------------
-template <bool HASH, int DK, int CK, bool OW1>
+// NZ = 8: one wave per brick (lane = (x, y) column, 8 z-steps).  NZ = 4 (dense only): two waves
+// per brick, one per z-half (zoff = 0 or 4) -- twice the waves for small culled lists (sharded
+// volumes), where one brick per wave leaves SIMDs idle, and half the per-lane registers.
+// 16-byte state halves (4 z-steps each) holding a set bit of `m` (bit k = step k of the part)
+template <int NZ>
+__device__ inline unsigned halves_of(unsigned m) {
+    return NZ == 8 ? (((m & 0x0Fu) ? 1u : 0u) | ((m & 0xF0u) ? 2u : 0u)) : (m ? 1u : 0u);
+}
+
+template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
-                                       const Table& tab, unsigned entry, unsigned long long* s_stat,
-                                       const double* s_rcp) {
+                                       const Table& tab, unsigned entry, int zoff,
+                                       unsigned long long* s_stat, const double* s_rcp) {
+    static_assert(NZ == 8 || (NZ == 4 && !HASH), "z-split parts are dense-only");
+    constexpr unsigned kHalves = NZ == 8 ? 3u : 1u;
     const int lane = lane_id();
     const int b = (int)(entry & 0xFFFFFFu);
     const unsigned fmask = entry >> 24;
     const int nb12 = v.nb[1] * v.nb[2];
+    if (b >= v.nb[0] * nb12) {  // never for a list k_cull wrote; guards the pool against bad input
+        if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
+        return;
+    }
     const int bx = b / nb12;
     const int rem = b - bx * nb12;
     const int by = rem / v.nb[2];
@@ -417,15 +432,15 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const int lx = bx * kBrickEdge + (lane >> 3);
     const int ly = by * kBrickEdge + (lane & 7);
     const bool col_in = lx < v.dims[0] && ly < v.dims[1];
-    const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge);
+    const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge) - zoff;  // valid steps of this part
     // vox2world (grid_fusion.py:170-181); lanes 0..7 compute the brick's 8 z coordinates
     const double px = vox_world(v.origin[0], v.vs, v.off[0] + bx * v.xstride + (lane >> 3));
     const double py = vox_world(v.origin[1], v.vs, v.off[1] + ly);
-    const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));
+    const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));  // lane k: z = k (zoff added at use)
 
-    float ws[kBrickEdge], ts[kBrickEdge], cs[kBrickEdge];
+    float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
-    for (int k = 0; k < kBrickEdge; ++k) {
+    for (int k = 0; k < NZ; ++k) {
         ws[k] = 0.0f;
         ts[k] = 1.0f;
         cs[k] = 0.0f;
@@ -449,11 +464,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
         // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
         // pixel lies within 1e-9 px of a rounding boundary are redone exactly afterwards.
-        double zc[kBrickEdge], uu[kBrickEdge], vv[kBrickEdge];
+        double zc[NZ], uu[NZ], vv[NZ];
         unsigned inb = 0, slow = 0;
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
-            const double pz = readlane_f64(pz_l, k);
+        for (int k = 0; k < NZ; ++k) {
+            const double pz = readlane_f64(pz_l, k + zoff);
             const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
@@ -471,9 +486,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }
         if (__ballot(slow != 0)) {
 #pragma unroll
-            for (int k = 0; k < kBrickEdge; ++k) {
+            for (int k = 0; k < NZ; ++k) {
                 if (!((slow >> k) & 1u)) continue;
-                const double pz = readlane_f64(pz_l, k);
+                const double pz = readlane_f64(pz_l, k + zoff);
                 const double x = fr.T[3] + fma(fr.T[2], pz, a0);
                 const double y = fr.T[7] + fma(fr.T[6], pz, a1);
                 uu[k] = rint((x * fr.fx) / zc[k] + fr.cx);  // the reference's own operation order
@@ -481,10 +496,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             }
         }
         unsigned cand = 0;
-        int pix[kBrickEdge];
+        int pix[NZ];
         const int W = fr.W, H = fr.H;
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
+        for (int k = 0; k < NZ; ++k) {
             const bool c = ((inb >> k) & 1u) && uu[k] >= 0.0 && uu[k] < (double)W &&
                            vv[k] >= 0.0 && vv[k] < (double)H;
             cand |= (unsigned)c << k;
@@ -495,21 +510,21 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
         // scheduling barrier keeps the compiler from sinking each load next to its use, which
         // under the 128-VGPR budget it otherwise does, serialising the latencies.
-        unsigned draw[kBrickEdge], cpx[kBrickEdge];
+        unsigned draw[NZ], cpx[NZ];
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
+        for (int k = 0; k < NZ; ++k) {
             draw[k] = depth_raw<DK>(fr, pix[k]);
             cpx[k] = (CK == 0) ? fr.rgbx[pix[k]] : __float_as_uint(((const float*)fr.color)[pix[k]]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        double dep[kBrickEdge];
+        double dep[NZ];
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) dep[k] = depth_m<DK>(fr, pix[k], draw[k]);
+        for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fr, pix[k], draw[k]);
         // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
         unsigned vmask = 0;
-        double dist[kBrickEdge];
+        double dist[NZ];
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
+        for (int k = 0; k < NZ; ++k) {
             const double diff = dep[k] - zc[k];
             const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
             const double dd = div_rn(diff, v.trunc, v.rtrunc);
@@ -533,7 +548,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     return;
                 }
                 blk = r;
-                if (is_new) loaded = 3u;  // a fresh block starts at (1, 0, 0): nothing to load
+                if (is_new) loaded = kHalves;  // a fresh block starts at (1, 0, 0): nothing to load
                 if (lane == 0) {
                     atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
                     atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
@@ -544,29 +559,21 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 blk = b;
             }
         }
-        const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge;
+        const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
         // phase 4: state halves not yet in registers, and the colour of every valid voxel
-        const unsigned need = ((vmask & 0x0Fu) ? 1u : 0u) | ((vmask & 0xF0u) ? 2u : 0u);
+        const unsigned need = halves_of<NZ>(vmask);
         const unsigned ld = need & ~loaded;
-        if (ld & 1u) {
-            const float4 W = *(const float4*)(pool.weight + base);
-            const float4 T = *(const float4*)(pool.tsdf + base);
-            const float4 C = *(const float4*)(pool.color + base);
-            ws[0] = W.x; ws[1] = W.y; ws[2] = W.z; ws[3] = W.w;
+#pragma unroll
+        for (int h = 0; h < NZ / 4; ++h) {
+            if (!((ld >> h) & 1u)) continue;
+            const float4 W = *(const float4*)(pool.weight + base + 4 * h);
+            const float4 T = *(const float4*)(pool.tsdf + base + 4 * h);
+            const float4 C = *(const float4*)(pool.color + base + 4 * h);
+            ws[4 * h + 0] = W.x; ws[4 * h + 1] = W.y; ws[4 * h + 2] = W.z; ws[4 * h + 3] = W.w;
             w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
             c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
-            ts[0] = T.x; ts[1] = T.y; ts[2] = T.z; ts[3] = T.w;
-            cs[0] = C.x; cs[1] = C.y; cs[2] = C.z; cs[3] = C.w;
-        }
-        if (ld & 2u) {
-            const float4 W = *(const float4*)(pool.weight + base + 4);
-            const float4 T = *(const float4*)(pool.tsdf + base + 4);
-            const float4 C = *(const float4*)(pool.color + base + 4);
-            ws[4] = W.x; ws[5] = W.y; ws[6] = W.z; ws[7] = W.w;
-            w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
-            c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
-            ts[4] = T.x; ts[5] = T.y; ts[6] = T.z; ts[7] = T.w;
-            cs[4] = C.x; cs[5] = C.y; cs[6] = C.z; cs[7] = C.w;
+            ts[4 * h + 0] = T.x; ts[4 * h + 1] = T.y; ts[4 * h + 2] = T.z; ts[4 * h + 3] = T.w;
+            cs[4 * h + 0] = C.x; cs[4 * h + 1] = C.y; cs[4 * h + 2] = C.z; cs[4 * h + 3] = C.w;
         }
         loaded |= need;
         dirty |= need;
@@ -580,10 +587,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // with RN32(1/wn) = f32(RN64(1/wn)) (checked for every table entry by the CPU tests).
         const bool fast_t = OW1 && s_rcp && __ballot(!w_small) == 0;
         const bool fast_c = CK == 0 && fast_t && __ballot(!c_canon) == 0;
-        float tq[kBrickEdge];
+        float tq[NZ];
         if (fast_t) {
 #pragma unroll
-            for (int k = 0; k < kBrickEdge; ++k) {
+            for (int k = 0; k < NZ; ++k) {
                 const float wn = ws[k] + 1.0f;
                 const double y = s_rcp[(int)wn];
                 const double num = (double)(ws[k] * ts[k]) + dist[k];
@@ -591,14 +598,14 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < kBrickEdge; ++k) {
+            for (int k = 0; k < NZ; ++k) {
                 const float wn = OW1 ? ws[k] + 1.0f : (float)((double)ws[k] + fr.ow);
                 const double num = (double)(ws[k] * ts[k]) + (OW1 ? dist[k] : fr.ow * dist[k]);
                 tq[k] = (float)(num / (double)wn);
             }
         }
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
+        for (int k = 0; k < NZ; ++k) {
             const bool ok = (vmask >> k) & 1u;
             const float w_old = ws[k];
             const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
@@ -651,19 +658,16 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     if (blk < 0) return;  // no frame of the batch updated this brick
 
     // phase 6: store the changed halves once (a new hash block is written whole: its init)
-    const unsigned st = dirty | ((HASH && is_new) ? 3u : 0u);
-    const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge;
-    if (st & 1u) {
-        *(float4*)(pool.weight + base) = make_float4(ws[0], ws[1], ws[2], ws[3]);
-        *(float4*)(pool.tsdf + base) = make_float4(ts[0], ts[1], ts[2], ts[3]);
-        *(float4*)(pool.color + base) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+    const unsigned st = dirty | ((HASH && is_new) ? kHalves : 0u);
+    const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
+#pragma unroll
+    for (int h = 0; h < NZ / 4; ++h) {
+        if (!((st >> h) & 1u)) continue;
+        *(float4*)(pool.weight + base + 4 * h) = make_float4(ws[4 * h], ws[4 * h + 1], ws[4 * h + 2], ws[4 * h + 3]);
+        *(float4*)(pool.tsdf + base + 4 * h) = make_float4(ts[4 * h], ts[4 * h + 1], ts[4 * h + 2], ts[4 * h + 3]);
+        *(float4*)(pool.color + base + 4 * h) = make_float4(cs[4 * h], cs[4 * h + 1], cs[4 * h + 2], cs[4 * h + 3]);
     }
-    if (st & 2u) {
-        *(float4*)(pool.weight + base + 4) = make_float4(ws[4], ws[5], ws[6], ws[7]);
-        *(float4*)(pool.tsdf + base + 4) = make_float4(ts[4], ts[5], ts[6], ts[7]);
-        *(float4*)(pool.color + base + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
-    }
-    if (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns the block this launch
+    if constexpr (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns the block this launch
         unsigned long long mine = 0;
 #pragma unroll
         for (int k = 0; k < kBrickEdge; ++k) {
@@ -743,7 +747,8 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, un
                 s_stat[ST_VISITED] = (unsigned long long)__popcll(m);
             }
             base = __shfl(base, 0);
-            if (fmask) list[base + __popcll(m & ((1ull << lane) - 1ull))] = e | (fmask << 24);
+            const unsigned idx = base + __popcll(m & ((1ull << lane) - 1ull));
+            if (fmask && idx < (unsigned)(v.nb[0] * v.nb[1] * v.nb[2])) list[idx] = e | (fmask << 24);
         }
     }
     __syncthreads();
@@ -754,7 +759,7 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, un
 // grid, all resident), so the work is spread evenly whatever the frames see.  `count` (device)
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
-template <bool HASH, int DK, int CK, bool OW1>
+template <bool HASH, int DK, int CK, bool OW1, int NZ = 8>
 #ifndef TSDF_INTEGRATE_ATTR
 #define TSDF_INTEGRATE_ATTR __attribute__((amdgpu_waves_per_eu(4)))  // <= 128 VGPRs: 4 waves/SIMD
 #endif
@@ -768,10 +773,12 @@ __global__ __launch_bounds__(kWG) TSDF_INTEGRATE_ATTR void k_integrate(Vol v, Ba
     if (OW1)
         for (int i = tid; i < kRcpTab; i += kWG) s_rcp[i] = 1.0 / (double)i;
     __syncthreads();
-    const int n = count ? (int)coh_load(count) : n_list;
+    constexpr int parts = 8 / NZ;  // waves per listed brick
+    const int n = (count ? (int)coh_load(count) : n_list) * parts;
     const int nw = gridDim.x * (kWG / 64);
     for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
-        integrate_brick<HASH, DK, CK, OW1>(v, bt, pool, tab, list[e], s_stat, OW1 ? s_rcp : nullptr);
+        integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
+                                               s_stat, OW1 ? s_rcp : nullptr);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
