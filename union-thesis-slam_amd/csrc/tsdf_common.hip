@@ -294,7 +294,13 @@ int Base::end_call(int flags) {
 
 int Base::launch_prep(const Batch& bt, int dk, int ck, int W, int H) {
     dim3 grid((W + 63) / 64, (H + 63) / 64, bt.n);
-    if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
+    bool vec = dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0;
+    for (int i = 0; i < bt.n && vec; ++i)  // 8-byte depth, 4-byte colour, 16-byte RGBX rows
+        vec = ((uintptr_t)bt.f[i].depth_src % 8 == 0) && ((uintptr_t)bt.f[i].color % 4 == 0) &&
+              ((uintptr_t)bt.f[i].rgbx % 16 == 0) && ((uintptr_t)bt.f[i].depth_mask % 8 == 0);
+    if (vec)
+        hipLaunchKernelGGL(k_prep_vec<0>, grid, dim3(512), 0, stream, bt, count);
+    else if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
         hipLaunchKernelGGL((k_prep<0, 0>), grid, dim3(1024), 0, stream, bt, count);
     else if (dk == TSDF_DEPTH_U16_MM)
         hipLaunchKernelGGL((k_prep<0, 1>), grid, dim3(1024), 0, stream, bt, count);
