@@ -89,6 +89,13 @@ __global__ void k_zero_u64(unsigned long long* p, int n) {
     if (i < n) p[i] = 0ull;
 }
 
+namespace {
+__global__ void k_fill_rcp(double* r) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < kRcpTab) r[i] = 1.0 / (double)i;  // IEEE division: RN(1/i) (r[0] = inf, unused)
+}
+}  // namespace
+
 int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
                double vs, double trunc) {
     int ndev = 0;
@@ -128,6 +135,10 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     TSDF_HIP(hipMalloc(&list, sizeof(unsigned) * (size_t)n_bricks));
     TSDF_HIP(hipMalloc(&count, sizeof(unsigned int) * 4));
     TSDF_HIP(hipMemsetAsync(count, 0, sizeof(unsigned int) * 4, stream));
+    TSDF_HIP(hipMalloc(&rcp, sizeof(double) * kRcpTab));
+    hipLaunchKernelGGL(k_fill_rcp, dim3((kRcpTab + 255) / 256), dim3(256), 0, stream, rcp);
+    TSDF_HIP(hipGetLastError());
+    vol.rcp = rcp;
     TSDF_HIP(hipMalloc(&stats, sizeof(unsigned long long) * kNStat * kStatSpread));
     TSDF_HIP(hipMemsetAsync(stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, stream));
     return TSDF_OK;
@@ -373,6 +384,8 @@ void Base::release() {
 
     if (list) (void)hipFree(list);
     if (count) (void)hipFree(count);
+    if (rcp) (void)hipFree(rcp);
+    rcp = nullptr;
     if (stats) (void)hipFree(stats);
     if (cstream) (void)hipStreamSynchronize(cstream);
     for (int k = 0; k < 2; ++k) {

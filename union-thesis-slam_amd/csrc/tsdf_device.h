@@ -40,6 +40,7 @@ struct Vol {
     float origin[3];
     double vs, trunc;
     double rtrunc;  // RN(1 / trunc), from the host's IEEE division (Markstein quotient, below)
+    const double* rcp;  // kRcpTab entries RN(1/n) in HBM (copied to LDS by k_integrate)
 };
 
 // Per-frame constants (by value).
@@ -770,8 +771,8 @@ __global__ __launch_bounds__(kWG) TSDF_INTEGRATE_ATTR void k_integrate(Vol v, Ba
     __shared__ double s_rcp[OW1 ? kRcpTab : 1];  // RN(1/n): weights are small integers when ow == 1
     const int tid = threadIdx.x;
     if (tid < kNStat) s_stat[tid] = 0;
-    if (OW1)
-        for (int i = tid; i < kRcpTab; i += kWG) s_rcp[i] = 1.0 / (double)i;
+    if (OW1)  // 32 KB table copied with 16-byte loads (computing it cost 16 f64 divisions per thread)
+        for (int i = tid; i < kRcpTab / 2; i += kWG) ((double2*)s_rcp)[i] = ((const double2*)v.rcp)[i];
     __syncthreads();
     constexpr int parts = 8 / NZ;  // waves per listed brick
     const int n = (count ? (int)coh_load(count) : n_list) * parts;

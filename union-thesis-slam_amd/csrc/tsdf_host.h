@@ -66,6 +66,7 @@ struct Base {
     int n_cu = 256;             // compute units of the device
     PyrLayout lay{};
     unsigned long long* stats = nullptr;  // kNStat x kStatSpread
+    double* rcp = nullptr;                // reciprocal table (Vol::rcp)
     long long frames = 0;
     Profiler prof;
     // Host-pointer frames (frame ingest): two device staging slots filled
