@@ -121,6 +121,21 @@ int tsdf_dense_integrate_batch(tsdf_dense_t* h, int n_frames, const void* depth,
 int tsdf_dense_get(tsdf_dense_t* h, float* tsdf, float* weight, float* color);
 int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf, const float* weight, const float* color);
 int tsdf_dense_sync(tsdf_dense_t* h);
+/* Mesh of the shard's tsdf at level 0 (get_mesh / get_point_cloud, grid_fusion.py:322-360; the
+ * reference runs skimage's marching_cubes_lewiner on the host).  extract runs marching cubes on
+ * the device and keeps the result in the handle; get_mesh copies it out: verts n_verts x 3 f32
+ * world coordinates (index-space vertex * voxel_size + origin, in f32 like NumPy), normals
+ * n_verts x 3 f32 unit (towards positive tsdf), colors n_verts x 3 uint8 r, g, b of the voxel at
+ * round(vertex) (grid_fusion.py:336-346), faces n_tris x 3 int32 vertex ids.  One vertex per
+ * grid edge whose end values straddle 0 (one below 0, one not), at the linear interpolation;
+ * vertices ordered by (voxel, axis) in C-order and shared by the cells around the edge.  Any
+ * output pointer may be NULL.  A shard is meshed on its own (no cells across shard borders). */
+int tsdf_dense_extract_mesh(tsdf_dense_t* h, int64_t* n_verts, int64_t* n_tris);
+int tsdf_dense_get_mesh(tsdf_dense_t* h, float* verts, float* normals, uint8_t* colors, int32_t* faces);
+/* The marching-cubes case table in use: tri[256][16] cube-edge ids (-1 padded; edge e joins the
+ * corners differing in bit e / 4 of the corner index, its lower corner's other two bits being
+ * e % 4 in increasing bit order), ntri[256] triangles per case.  Host-only; no device needed. */
+int tsdf_mc_table(int8_t* tri, uint8_t* ntri);
 int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset);
 int tsdf_dense_set_profiling(tsdf_dense_t* h, int on);
 

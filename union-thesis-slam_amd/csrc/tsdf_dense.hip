@@ -10,6 +10,7 @@ using namespace tsdf;
 
 struct tsdf_dense {
     Base b;
+    Mesh mesh;
     int nz = 4;  // z-steps per wave in k_integrate (8: a brick per wave; 4: a z-half per wave)
 };
 
@@ -197,6 +198,7 @@ int tsdf_dense_create_shard(const int64_t global_dims[3], int shard, int n_shard
 int tsdf_dense_destroy(tsdf_dense_t* h) {
     if (!h) return TSDF_OK;
     (void)hipSetDevice(h->b.device);
+    h->mesh.release();
     h->b.release();
     if (h->b.pool.tsdf) (void)hipFree(h->b.pool.tsdf);
     if (h->b.pool.weight) (void)hipFree(h->b.pool.weight);
@@ -260,6 +262,21 @@ int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
     return h->b.read_stats(out, reset);
+}
+
+int tsdf_dense_extract_mesh(tsdf_dense_t* h, int64_t* n_verts, int64_t* n_tris) {
+    if (!h || !n_verts || !n_tris) return set_error(TSDF_E_ARG, "null pointer");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(extract_mesh(h->b, h->b.pool, h->mesh));
+    *n_verts = h->mesh.n_verts;
+    *n_tris = h->mesh.n_tris;
+    return TSDF_OK;
+}
+
+int tsdf_dense_get_mesh(tsdf_dense_t* h, float* verts, float* normals, uint8_t* colors, int32_t* faces) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    return copy_mesh(h->b, h->mesh, verts, normals, colors, faces);
 }
 
 int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {

@@ -113,6 +113,18 @@ struct Base {
     void release();
 };
 
+// An extracted mesh, in device memory (tsdf_mesh.hip).
+struct Mesh {
+    float* verts = nullptr;           // n_verts x 3 world coordinates
+    float* normals = nullptr;         // n_verts x 3 unit normals (to positive tsdf)
+    unsigned char* colors = nullptr;  // n_verts x 3 uint8 r, g, b
+    int* faces = nullptr;             // n_tris x 3 vertex ids
+    long long n_verts = 0, n_tris = 0;
+    void release();
+};
+int extract_mesh(Base& B, const Pool& pool, Mesh& m);
+int copy_mesh(Base& B, const Mesh& m, float* verts, float* normals, uint8_t* colors, int32_t* faces);
+
 // end_call on every exit path of an integrate call (error returns included).
 struct CallGuard {
     Base& b;

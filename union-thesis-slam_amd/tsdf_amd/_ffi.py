@@ -68,6 +68,9 @@ SIGNATURES = {
     "tsdf_device_count": [_P],
     "tsdf_dense_create": [_P, _P, _P, _D, _D, _I, _P],
     "tsdf_dense_create_shard": [_P, _I, _I, _P, _D, _D, _I, _P],
+    "tsdf_dense_extract_mesh": [_P, _P, _P],
+    "tsdf_dense_get_mesh": [_P, _P, _P, _P, _P],
+    "tsdf_mc_table": [_P, _P],
     "tsdf_frustum_bounds": [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P],
     "tsdf_dense_destroy": [_P],
     "tsdf_dense_reset": [_P],

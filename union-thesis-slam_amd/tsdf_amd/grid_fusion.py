@@ -18,6 +18,7 @@ import ctypes
 import numpy as np
 
 from . import _ffi, sharding
+from .ply import meshwrite, pcwrite  # noqa: F401  (grid_fusion.meshwrite / pcwrite, as in the reference)
 
 
 def volume_geometry(vol_bnds, voxel_size):
@@ -202,11 +203,27 @@ class TSDFVolume:
     def reset(self):
         _ffi.call("tsdf_dense_reset", self._h)
 
+    def extract_mesh(self, normals=True, colors=True, faces=True):
+        """Marching cubes at level 0 on the device (tsdf_dense_extract_mesh): (verts (N,3) f32
+        world, normals (N,3) f32, colors (N,3) u8, faces (M,3) i32); a field not asked for is None."""
+        nv, nt = ctypes.c_int64(), ctypes.c_int64()
+        _ffi.call("tsdf_dense_extract_mesh", self._h, ctypes.byref(nv), ctypes.byref(nt))
+        v = np.empty((nv.value, 3), np.float32)
+        n = np.empty((nv.value, 3), np.float32) if normals else None
+        c = np.empty((nv.value, 3), np.uint8) if colors else None
+        f = np.empty((nt.value, 3), np.int32) if faces else None
+        _ffi.call("tsdf_dense_get_mesh", self._h, _ffi.ptr(v), _ffi.ptr(n), _ffi.ptr(c), _ffi.ptr(f))
+        return v, n, c, f
+
     def get_point_cloud(self):
-        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+        """grid_fusion.py:322-338: (N, 6) float32 rows x, y, z, r, g, b of the mesh vertices."""
+        v, _, c, _ = self.extract_mesh(normals=False, faces=False)
+        return np.hstack([v, c])
 
     def get_mesh(self):
-        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+        """grid_fusion.py:340-360: (verts, faces, norms, colors) from marching cubes on the device."""
+        v, n, c, f = self.extract_mesh()
+        return v, f, n, c
 
     def close(self):
         if getattr(self, "_h", None):

@@ -21,7 +21,9 @@ factor and collisions are counted over block slots, not 5-voxel buckets.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import io
 
 import numpy as np
 
@@ -227,11 +229,23 @@ class HashTable:
         _ffi.call("tsdf_hash_get_dense", self._h, _ffi.ptr(t), _ffi.ptr(w), _ffi.ptr(c))
         return t, w, c
 
+    def _as_grid(self):
+        """The densified volume (get_volume, hash_fusion.py:442-463) in a dense device handle."""
+        t, w, c = self.get_state()
+        lo = np.asarray(self._vol_bounds, dtype=np.float64)[:, 0]
+        bnds = np.stack([lo, lo + (np.asarray(self._vol_dim) - 0.5) * self._voxel_size], axis=1)  # same dims
+        with contextlib.redirect_stdout(io.StringIO()):
+            vol = grid_fusion.TSDFVolume(bnds, self._voxel_size, device=self.device)
+        vol.set_state(t, w, c)
+        return vol
+
     def get_mesh(self):
-        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+        """hash_fusion.py:465-484: marching cubes of the densified volume, on the device."""
+        return self._as_grid().get_mesh()
 
     def get_point_cloud(self):
-        raise NotImplementedError("marching cubes extraction is SURVEY §8(f) next-row 1 (not built yet)")
+        """hash_fusion.py:486-507."""
+        return self._as_grid().get_point_cloud()
 
     # ------------------------------------------------------------------ misc
     def sync(self):
