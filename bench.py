@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host-frame (PCIe) measurement")
     ap.add_argument("--ingest-frames", type=int, default=256)
+    ap.add_argument("--no-mesh", action="store_true", help="skip the mesh-extraction measurement")
     return ap.parse_args()
 
 
@@ -199,6 +200,20 @@ def main():
                             "device slots overlapped with integrate (tsdf_dense_integrate_batch "
                             "without TSDF_DEVICE_PTRS)"}
         log(f"[rank {rank}] ingest: {ni} host frames in {ti * 1e3:.1f} ms -> {ni / ti:.0f} frames/s")
+    # ---- mesh extraction of the fused volume (not part of `value`) ----
+    mesh = None
+    if not args.no_mesh and rank == 0:
+        import ctypes
+        nv, nt = ctypes.c_int64(), ctypes.c_int64()
+        sync()
+        t0 = time.perf_counter()
+        _ffi.call("tsdf_dense_extract_mesh", vol._h, ctypes.byref(nv), ctypes.byref(nt))
+        tm = time.perf_counter() - t0
+        nvox = len(vol.x_index) * X * X
+        mesh = {"ms": round(1e3 * tm, 2), "vertices": nv.value, "triangles": nt.value,
+                "mvoxels_per_s": round(nvox / tm / 1e6, 1),
+                "note": "marching cubes on the device over the rank's shard after the timed run"}
+        log(f"[rank {rank}] mesh: {nv.value} vertices, {nt.value} triangles in {tm * 1e3:.1f} ms")
     del vol
     torch.cuda.empty_cache()
 
@@ -262,6 +277,7 @@ def main():
             "mean_voxels_updated_per_frame": round(vox / Kt),
             "hash": hash_res,
             "pcie_inclusive": ingest,
+            "mesh": mesh,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -1,7 +1,9 @@
 // tsdf_common.hip -- errors, device discovery, frame staging, pyramid launch, profiling and
 // the bulk hash_function entry point of the C-ABI (include/tsdf_hip.h).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <thread>
 
 #include "tsdf_host.h"
 
@@ -129,7 +131,8 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     for (int k = 0; k < 2; ++k) {
         TSDF_HIP(hipEventCreateWithFlags(&ev_copied[k], hipEventDisableTiming));
         TSDF_HIP(hipEventCreateWithFlags(&ev_free[k], hipEventDisableTiming));
-        TSDF_HIP(hipEventRecord(ev_free[k], stream));  // both slots start free
+        TSDF_HIP(hipEventRecord(ev_free[k], stream));      // both slots start free
+        TSDF_HIP(hipEventRecord(ev_copied[k], cstream));
     }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
     TSDF_HIP(hipMalloc(&list, sizeof(unsigned) * (size_t)n_bricks));
@@ -194,6 +197,24 @@ static void frustum_planes(Frame* fr, const double* T, int W, int H) {
     }
 }
 
+// memcpy with up to 8 threads (host bounce copies run at several times one core's bandwidth)
+static void par_memcpy(void* dst, const void* src, size_t bytes) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nt = bytes < (4u << 20) ? 1 : std::min<size_t>(8, hw ? hw : 1);
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t chunk = (bytes + nt - 1) / nt;
+    for (size_t i = 0; i < nt; ++i) {
+        const size_t o = i * chunk;
+        if (o >= bytes) break;
+        th.emplace_back([=] { std::memcpy((char*)dst + o, (const char*)src + o, std::min(chunk, bytes - o)); });
+    }
+    for (auto& t : th) t.join();
+}
+
 int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
                         int W, const double K[9], const double* Tinv, const double* ow,
                         double ow_default, int flags, int first, int n) {
@@ -211,19 +232,27 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
             for (int k = 0; k < 2; ++k) {
                 if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
                 if (st_color[k]) TSDF_HIP(hipFree(st_color[k]));
-                st_depth[k] = st_color[k] = nullptr;
+                if (hst_depth[k]) TSDF_HIP(hipHostFree(hst_depth[k]));
+                if (hst_color[k]) TSDF_HIP(hipHostFree(hst_color[k]));
+                st_depth[k] = st_color[k] = hst_depth[k] = hst_color[k] = nullptr;
             }
             st_depth_bytes = st_color_bytes = 0;
             for (int k = 0; k < 2; ++k) {
                 TSDF_HIP(hipMalloc(&st_depth[k], dbytes * kMaxBatch));
                 TSDF_HIP(hipMalloc(&st_color[k], cbytes * kMaxBatch));
+                TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * kMaxBatch, hipHostMallocDefault));
+                TSDF_HIP(hipHostMalloc(&hst_color[k], cbytes * kMaxBatch, hipHostMallocDefault));
             }
             st_depth_bytes = dbytes * kMaxBatch;
             st_color_bytes = cbytes * kMaxBatch;
         }
+        // the bounce slot is free once its previous DMA has finished
+        TSDF_HIP(hipEventSynchronize(ev_copied[slot]));
+        par_memcpy(hst_depth[slot], d, dbytes * n);
+        par_memcpy(hst_color[slot], c, cbytes * n);
         TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[slot], 0));
-        TSDF_HIP(hipMemcpyAsync(st_depth[slot], d, dbytes * n, hipMemcpyHostToDevice, cstream));
-        TSDF_HIP(hipMemcpyAsync(st_color[slot], c, cbytes * n, hipMemcpyHostToDevice, cstream));
+        TSDF_HIP(hipMemcpyAsync(st_depth[slot], hst_depth[slot], dbytes * n, hipMemcpyHostToDevice, cstream));
+        TSDF_HIP(hipMemcpyAsync(st_color[slot], hst_color[slot], cbytes * n, hipMemcpyHostToDevice, cstream));
         TSDF_HIP(hipEventRecord(ev_copied[slot], cstream));
         TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
         d = (const char*)st_depth[slot];
@@ -267,23 +296,9 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
     return TSDF_OK;
 }
 
-// Page-lock [p, p + bytes) for the call unless it is already device-visible host memory.
-static int pin_range(std::vector<const void*>& pinned, const void* p, size_t bytes) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type != hipMemoryTypeUnregistered)
-        return TSDF_OK;  // pinned, registered or device memory already
-    (void)hipGetLastError();
-    const hipError_t e = hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault);
-    if (e == hipSuccess) pinned.push_back(p);
-    else (void)hipGetLastError();  // not registrable: hipMemcpyAsync still copies (staged)
-    return TSDF_OK;
-}
-
 int Base::begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags) {
+    (void)depth, (void)dbytes, (void)color, (void)cbytes, (void)flags;
     call_batch = 0;
-    if (flags & TSDF_DEVICE_PTRS) return TSDF_OK;
-    TSDF_TRY(pin_range(pinned, depth, dbytes));
-    if (color != depth) TSDF_TRY(pin_range(pinned, color, cbytes));
     return TSDF_OK;
 }
 
@@ -294,12 +309,7 @@ int Base::end_batch(int flags) {
 }
 
 int Base::end_call(int flags) {
-    if (flags & TSDF_DEVICE_PTRS) return TSDF_OK;
-    // the caller's host arrays are borrowed for the call: every copy has landed before return
-    const hipError_t e = hipStreamSynchronize(cstream);
-    for (const void* p : pinned) (void)hipHostUnregister(const_cast<void*>(p));
-    pinned.clear();
-    TSDF_HIP(e);
+    (void)flags;  // the host arrays were fully read into the bounce slots before this point
     return TSDF_OK;
 }
 
@@ -398,8 +408,11 @@ void Base::release() {
     }
     if (dmask) (void)hipFree(dmask);
     dmask = nullptr;
-    for (const void* p : pinned) (void)hipHostUnregister(const_cast<void*>(p));
-    pinned.clear();
+    for (int k = 0; k < 2; ++k) {
+        if (hst_depth[k]) (void)hipHostFree(hst_depth[k]);
+        if (hst_color[k]) (void)hipHostFree(hst_color[k]);
+        hst_depth[k] = hst_color[k] = nullptr;
+    }
     if (cstream) (void)hipStreamDestroy(cstream);
     cstream = nullptr;
     if (stream) (void)hipStreamDestroy(stream);

@@ -69,10 +69,10 @@ struct Base {
     double* rcp = nullptr;                // reciprocal table (Vol::rcp)
     long long frames = 0;
     Profiler prof;
-    // Host-pointer frames (frame ingest): two device staging slots filled
-    // by DMA on a copy stream while the compute stream integrates the other slot's batch.
-    // The caller's host arrays are page-locked for the call (hipHostRegister) when they are
-    // not already, so the copies are true asynchronous DMA.
+    // Host-pointer frames (frame ingest): the host copies each batch (with
+    // several threads) into one of two page-locked bounce slots, a copy stream DMAs it into the
+    // matching device staging slot, and the compute stream integrates it -- while the host
+    // already fills the other slot.
     hipStream_t cstream = nullptr;
     hipEvent_t ev_copied[2] = {nullptr, nullptr};  // slot's frames landed (copy stream)
     hipEvent_t ev_free[2] = {nullptr, nullptr};    // slot's last reader finished (compute stream)
@@ -82,7 +82,8 @@ struct Base {
     unsigned short* dmask = nullptr;  // kMaxBatch masked u16 depth images (TSDF_DEPTH_INVALID_65535)
     size_t dmask_px = 0;
     long long call_batch = 0;         // batches issued in the current call
-    std::vector<const void*> pinned;  // ranges this call registered (unregistered by end_call)
+    void* hst_depth[2] = {nullptr, nullptr};  // page-locked bounce slots (hipHostMalloc)
+    void* hst_color[2] = {nullptr, nullptr};
 
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
@@ -92,9 +93,10 @@ struct Base {
     int prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
                       int W, const double K[9], const double* Tinv, const double* ow,
                       double ow_default, int flags, int first, int n);
-    // Around the batches of one integrate call: begin_call pins the caller's host arrays (if
-    // host pointers), end_batch marks the batch's staging slot reusable once the compute stream
-    // has finished with it, end_call waits for the copies and unpins.
+    // Around the batches of one integrate call: end_batch marks the batch's staging slot
+    // reusable once the compute stream has finished with it.  begin_call / end_call bracket the
+    // call (the caller's host arrays are read synchronously into the bounce slots, so nothing
+    // of them is held past the call).
     int begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags);
     int end_batch(int flags);
     int end_call(int flags);
