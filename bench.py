@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-ingest", action="store_true", help="skip the host-frame (PCIe) measurement")
     ap.add_argument("--ingest-frames", type=int, default=256)
     ap.add_argument("--no-mesh", action="store_true", help="skip the mesh-extraction measurement")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: several ranks may share a GPU)")
     return ap.parse_args()
 
 
@@ -103,10 +105,15 @@ def main():
     if args.gpus != world and world > 1:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     n = world
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local if args.dist_backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if n > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     def barrier():
         if n > 1:
@@ -118,14 +125,14 @@ def main():
     def max_over_ranks(x):
         if n == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_over_ranks(x):
         if n == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
@@ -152,7 +159,7 @@ def main():
     bnds = np.array([[0.0, ROOM]] * 3)
     import contextlib
     with contextlib.redirect_stdout(sys.stderr):  # the reference-style ctor prints; keep stdout JSON-only
-        vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=local, shard=(rank, n))
+        vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=gpu, shard=(rank, n))
     W, Kt = args.warmup, args.steps
     run_timed(vol, depth, rgb, K, Tinv, 0, W, F, sync, barrier, False)
     dt = run_timed(vol, depth, rgb, K, Tinv, W, Kt, F, sync, barrier, not args.no_profile)
@@ -222,7 +229,7 @@ def main():
     if not args.no_hash:
         nb = (X // 8) ** 3
         with contextlib.redirect_stdout(sys.stderr):
-            ht = hash_fusion.HashTable(np.array([[0.0, ROOM]] * 3), VOXEL, 1 << 22, device=local,
+            ht = hash_fusion.HashTable(np.array([[0.0, ROOM]] * 3), VOXEL, 1 << 22, device=gpu,
                                        max_blocks=nb, shard=rank, n_shards=n)
         run_timed(ht, depth, rgb, K, Tinv, 0, W, F, sync, barrier, False)
         hdt = run_timed(ht, depth, rgb, K, Tinv, W, Kt, F, sync, barrier, not args.no_profile)
