@@ -312,3 +312,38 @@ def test_invalid_65535_mask_on_device(gf):
     vol2 = gf.TSDFVolume(bnds.copy(), 0.04)
     vol2.integrate_batch(raw, rgb, K, np.linalg.inv(poses))
     assert not _same(vol2.get_state()[1], W)
+
+
+@pytest.mark.parametrize("ingest", ["device", "host"])
+def test_prep_cull_pipeline_on_and_off_bit_identical(gf, monkeypatch, ingest):
+    """Small volumes pipeline prep + cull of batch k+1 with integrate k on a second stream and a
+    second buffer set (tsdf_dense.hip); large ones run them in line.  Both paths,
+    forced with TSDF_PIPELINE, over 29 async frames (4 batches, both sets reused) with 65535
+    masking, equal each other and the oracle bit for bit."""
+    import torch
+    d, c, poses = _synth(29, start=11)
+    d = np.ascontiguousarray(d).astype(np.uint16)
+    d[3:9, 50:90, 100:200] = 65535
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    bnds = np.array([[0.0, 10.24]] * 3)
+    Tinv = np.linalg.inv(poses)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
+    dm = np.where(d == 65535, 0, d)
+    n = sum(orc.integrate(c[f], dm[f].astype(float) / 1000.0, K, poses[f]) for f in range(len(d)))
+    states = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("TSDF_PIPELINE", pipe)
+        vol = gf.TSDFVolume(bnds.copy(), 0.08)
+        if ingest == "host":
+            vol.integrate_batch(d, np.ascontiguousarray(c), K, Tinv, sync=False, invalid_65535=True)
+        else:
+            dd, cc = torch.from_numpy(d.view(np.int16)).cuda(), torch.from_numpy(np.ascontiguousarray(c)).cuda()
+            torch.cuda.synchronize()
+            vol.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True,
+                                sync=False, invalid_65535=True)
+        vol.sync()
+        st = vol.stats()
+        assert st["voxel_updates"] == n and st["list_errors"] == 0
+        states.append(vol.get_state())
+    for a, b, e in zip(states[0], states[1], (orc._tsdf_vol_cpu, orc._weight_vol_cpu, orc._color_vol_cpu)):
+        assert _same(a, e) and _same(b, e)

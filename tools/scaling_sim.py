@@ -65,8 +65,9 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(r, world))
         timed(vol, 0, a.warmup)
+        vol.stats(reset=True)
         t = timed(vol, a.warmup, a.steps)
-        print(json.dumps({"only": a.only, "fps": round(a.steps / t, 1)}))
+        print(json.dumps({"only": a.only, "fps": round(a.steps / t, 1), "stats": vol.stats()}, default=float))
         return
     for world in [int(w) for w in a.worlds.split(",")]:
         for mode in ("slab", "cyclic"):

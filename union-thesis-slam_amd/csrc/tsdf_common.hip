@@ -135,9 +135,10 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
         TSDF_HIP(hipEventRecord(ev_copied[k], cstream));
     }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    TSDF_HIP(hipMalloc(&list, sizeof(unsigned) * (size_t)n_bricks));
-    TSDF_HIP(hipMalloc(&count, sizeof(unsigned int) * 4));
-    TSDF_HIP(hipMemsetAsync(count, 0, sizeof(unsigned int) * 4, stream));
+    TSDF_HIP(hipMalloc(&list_set[0], sizeof(unsigned) * (size_t)n_bricks));
+    TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * 4));
+    TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * 4, stream));
+    use_set(0);
     TSDF_HIP(hipMalloc(&rcp, sizeof(double) * kRcpTab));
     hipLaunchKernelGGL(k_fill_rcp, dim3((kRcpTab + 255) / 256), dim3(256), 0, stream, rcp);
     TSDF_HIP(hipGetLastError());
@@ -147,21 +148,61 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     return TSDF_OK;
 }
 
-int Base::ensure_pyr(int H, int W) {
-    if (pyr && H == pyr_H && W == pyr_W) return TSDF_OK;
-    if (pyr) {
-        TSDF_HIP(hipStreamSynchronize(stream));
-        TSDF_HIP(hipFree(pyr));
-        TSDF_HIP(hipFree(rgbx));
-        pyr = nullptr;
-        rgbx = nullptr;
+// Second buffer set + prep stream: prep and cull of batch k+1 overlap integrate k.  Pays off when
+// the integrate is short (a shard of a multi-GPU volume): there the fixed-latency prep/cull
+// would otherwise leave the GPU idle between integrates.  On a full volume the overlapping
+// kernels only take CUs from the integrate, so the caller decides.
+int Base::enable_pipeline() {
+    if (pipe) return TSDF_OK;
+    int least = 0, greatest = 0;
+    TSDF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* pe = getenv("TSDF_PIPE_PRIO");
+    const int prio = pe ? atoi(pe) : 1;
+    if (prio >= 1) {  // prep/cull fill the CUs the integrate leaves (its tail) instead of sharing them
+        TSDF_HIP(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, least));
+    } else {
+        TSDF_HIP(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
     }
+    if (prio >= 2) {
+        TSDF_HIP(hipStreamDestroy(stream));
+        TSDF_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, greatest));
+    }
+    for (int k = 0; k < 2; ++k) {
+        TSDF_HIP(hipEventCreateWithFlags(&ev_culled[k], hipEventDisableTiming));
+        TSDF_HIP(hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming));
+        TSDF_HIP(hipEventRecord(ev_done[k], stream));
+    }
+    TSDF_HIP(hipMalloc(&list_set[1], sizeof(unsigned) * (size_t)n_bricks));
+    TSDF_HIP(hipMalloc(&count_set[1], sizeof(unsigned int) * 4));
+    TSDF_HIP(hipMemsetAsync(count_set[1], 0, sizeof(unsigned int) * 4, stream));
+    TSDF_HIP(hipStreamSynchronize(stream));
+    pipe = true;
+    return TSDF_OK;
+}
 
+int Base::sync_all() {
+    TSDF_HIP(hipStreamSynchronize(stream));
+    if (pstream) TSDF_HIP(hipStreamSynchronize(pstream));
+    return TSDF_OK;
+}
+
+int Base::ensure_pyr(int H, int W) {
+    if (pyr_set[0] && H == pyr_H && W == pyr_W && (!pipe || pyr_set[1])) return TSDF_OK;
+    TSDF_TRY(sync_all());
+    for (int k = 0; k < 2; ++k) {
+        if (pyr_set[k]) TSDF_HIP(hipFree(pyr_set[k]));
+        if (rgbx_set[k]) TSDF_HIP(hipFree(rgbx_set[k]));
+        pyr_set[k] = nullptr;
+        rgbx_set[k] = nullptr;
+    }
     lay = pyr_layout(H, W);
-    TSDF_HIP(hipMalloc(&pyr, sizeof(float) * (size_t)lay.total * kMaxBatch));
-    TSDF_HIP(hipMalloc(&rgbx, sizeof(unsigned) * (size_t)H * W * kMaxBatch));
+    for (int k = 0; k < (pipe ? 2 : 1); ++k) {
+        TSDF_HIP(hipMalloc(&pyr_set[k], sizeof(float) * (size_t)lay.total * kMaxBatch));
+        TSDF_HIP(hipMalloc(&rgbx_set[k], sizeof(unsigned) * (size_t)H * W * kMaxBatch));
+    }
     pyr_H = H;
     pyr_W = W;
+    use_set(pipe ? (int)(batches & 1) : 0);
     return TSDF_OK;
 }
 
@@ -227,7 +268,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
     if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames into slot call_batch & 1
         const int slot = (int)(call_batch & 1);
         if (st_depth_bytes < dbytes * kMaxBatch || st_color_bytes < cbytes * kMaxBatch) {
-            TSDF_HIP(hipStreamSynchronize(stream));
+            TSDF_TRY(sync_all());
             TSDF_HIP(hipStreamSynchronize(cstream));
             for (int k = 0; k < 2; ++k) {
                 if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
@@ -254,17 +295,22 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         TSDF_HIP(hipMemcpyAsync(st_depth[slot], hst_depth[slot], dbytes * n, hipMemcpyHostToDevice, cstream));
         TSDF_HIP(hipMemcpyAsync(st_color[slot], hst_color[slot], cbytes * n, hipMemcpyHostToDevice, cstream));
         TSDF_HIP(hipEventRecord(ev_copied[slot], cstream));
-        TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
+        TSDF_HIP(hipStreamWaitEvent(prep_stream(), ev_copied[slot], 0));
+        if (pipe) TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
         d = (const char*)st_depth[slot];
         c = (const char*)st_color[slot];
     }
     const bool mask = (flags & TSDF_DEPTH_INVALID_65535) && dk == TSDF_DEPTH_U16_MM;
-    if (mask && dmask_px < npx) {
-        TSDF_HIP(hipStreamSynchronize(stream));
-        if (dmask) TSDF_HIP(hipFree(dmask));
-        dmask = nullptr;
-        TSDF_HIP(hipMalloc(&dmask, sizeof(unsigned short) * npx * kMaxBatch));
+    if (mask && (dmask_px < npx || (pipe && !dmask_set[1]))) {
+        TSDF_TRY(sync_all());
+        for (int k = 0; k < 2; ++k) {
+            if (dmask_set[k]) TSDF_HIP(hipFree(dmask_set[k]));
+            dmask_set[k] = nullptr;
+        }
+        for (int k = 0; k < (pipe ? 2 : 1); ++k)
+            TSDF_HIP(hipMalloc(&dmask_set[k], sizeof(unsigned short) * npx * kMaxBatch));
         dmask_px = npx;
+        use_set(pipe ? (int)(batches & 1) : 0);
     }
     bt->n = n;
     for (int i = 0; i < n; ++i) {
@@ -313,7 +359,7 @@ int Base::end_call(int flags) {
     return TSDF_OK;
 }
 
-int Base::launch_prep(const Batch& bt, int dk, int ck, int W, int H) {
+int Base::launch_prep(const Batch& bt, int dk, int ck, int W, int H, hipStream_t stream) {
     dim3 grid((W + 63) / 64, (H + 63) / 64, bt.n);
     bool vec = dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0;
     for (int i = 0; i < bt.n && vec; ++i)  // 8-byte depth, 4-byte colour, 16-byte RGBX rows
@@ -388,12 +434,26 @@ int Base::set_profiling(int on) {
 
 void Base::release() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (pstream) (void)hipStreamSynchronize(pstream);
     prof.release();
-    if (pyr) (void)hipFree(pyr);
-    if (rgbx) (void)hipFree(rgbx);
-
-    if (list) (void)hipFree(list);
-    if (count) (void)hipFree(count);
+    for (int k = 0; k < 2; ++k) {
+        if (pyr_set[k]) (void)hipFree(pyr_set[k]);
+        if (rgbx_set[k]) (void)hipFree(rgbx_set[k]);
+        if (list_set[k]) (void)hipFree(list_set[k]);
+        if (count_set[k]) (void)hipFree(count_set[k]);
+        if (dmask_set[k]) (void)hipFree(dmask_set[k]);
+        if (ev_culled[k]) (void)hipEventDestroy(ev_culled[k]);
+        if (ev_done[k]) (void)hipEventDestroy(ev_done[k]);
+        pyr_set[k] = nullptr;
+        rgbx_set[k] = nullptr;
+        list_set[k] = nullptr;
+        count_set[k] = nullptr;
+        dmask_set[k] = nullptr;
+        ev_culled[k] = ev_done[k] = nullptr;
+    }
+    if (pstream) (void)hipStreamDestroy(pstream);
+    pstream = nullptr;
+    pipe = false;
     if (rcp) (void)hipFree(rcp);
     rcp = nullptr;
     if (stats) (void)hipFree(stats);
@@ -406,7 +466,6 @@ void Base::release() {
         st_depth[k] = st_color[k] = nullptr;
         ev_copied[k] = ev_free[k] = nullptr;
     }
-    if (dmask) (void)hipFree(dmask);
     dmask = nullptr;
     for (int k = 0; k < 2; ++k) {
         if (hst_depth[k]) (void)hipHostFree(hst_depth[k]);

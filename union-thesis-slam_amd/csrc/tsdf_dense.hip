@@ -56,11 +56,20 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+        const int set = B.pipe ? (int)(B.batches & 1) : 0;
+        B.use_set(set);
         TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, ow, 1.0, flags, f0, n));
-        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H));
-        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, no_table,
+        const hipStream_t ps = B.prep_stream();
+        // pipelined: the set's previous integrate (batch k-2) must be done before prep overwrites it
+        if (B.pipe) TSDF_HIP(hipStreamWaitEvent(ps, B.ev_done[set], 0));
+        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, ps));
+        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kCullWG), 0, ps, B.vol, bt, no_table,
                            B.list, B.count, B.stats);
         TSDF_HIP(hipGetLastError());
+        if (B.pipe) {
+            TSDF_HIP(hipEventRecord(B.ev_culled[set], ps));
+            TSDF_HIP(hipStreamWaitEvent(B.stream, B.ev_culled[set], 0));
+        }
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
         bool ow1 = true;
@@ -94,8 +103,10 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
         }
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
+        if (B.pipe) TSDF_HIP(hipEventRecord(B.ev_done[set], B.stream));
         TSDF_TRY(B.end_batch(flags));
         B.frames += n;
+        ++B.batches;
     }
     TSDF_TRY(guard.finish());
     if (!(flags & TSDF_ASYNC)) TSDF_HIP(hipStreamSynchronize(B.stream));
@@ -150,6 +161,13 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
         }
         const int64_t gx_max = (int64_t)h->b.vol.off[0] + (int64_t)(h->b.vol.nb[0] - 1) * xstride + kBrickEdge;
         if (gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
+    }
+    if (r == TSDF_OK) {
+        // prep/cull pipeline: on for small volumes (the integrate is then short),
+        // TSDF_PIPELINE=0/1 overrides
+        bool pipe = h->b.n_bricks <= kPipelineMaxBricks;
+        if (const char* e = getenv("TSDF_PIPELINE")) pipe = atoi(e) != 0;
+        if (pipe) r = h->b.enable_pipeline();
     }
     if (r == TSDF_OK) {
         const size_t n = (size_t)h->b.n_bricks * kBrickVox * sizeof(float);

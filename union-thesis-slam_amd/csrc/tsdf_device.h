@@ -455,9 +455,15 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
     bool c_canon = true;   // all loaded colours are canonical (canon_color)
 
+#ifdef TSDF_DIAG
+    int d_pairs = 0, d_valid = 0;
+#endif
     for (int fi = 0; fi < bt.n; ++fi) {
         if (!((fmask >> fi) & 1u)) continue;
         const Frame& fr = bt.f[fi];
+#ifdef TSDF_DIAG
+        ++d_pairs;
+#endif
         // x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:363-368)
         const double a0 = fma(fr.T[1], py, fr.T[0] * px);
         const double a1 = fma(fr.T[5], py, fr.T[4] * px);
@@ -533,6 +539,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             vmask |= (unsigned)ok << k;
         }
         if (__ballot(vmask != 0) == 0) continue;
+#ifdef TSDF_DIAG
+        ++d_valid;
+#endif
 
         if (blk < 0) {  // first frame of the batch that updates this brick: find its storage
             if (HASH) {
@@ -656,6 +665,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             nupd += ok ? 1 : 0;
         }
     }
+#ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
+    if (!HASH && lane == 0) {
+        atomicAdd(&s_stat[ST_PROBE], (unsigned long long)d_pairs);
+        atomicAdd(&s_stat[ST_LOOKUPS], (unsigned long long)d_valid);
+    }
+#endif
     if (blk < 0) return;  // no frame of the batch updated this brick
 
     // phase 6: store the changed halves once (a new hash block is written whole: its init)

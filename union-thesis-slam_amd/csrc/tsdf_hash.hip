@@ -390,7 +390,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
         TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, nullptr, 1.0, flags, f0, n));
-        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H));
+        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, B.stream));
         hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, h->t, B.list,
                            B.count, B.stats);
         TSDF_HIP(hipGetLastError());

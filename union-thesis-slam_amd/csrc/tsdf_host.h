@@ -51,6 +51,10 @@ struct Profiler {
     void release();
 };
 
+// Dense handles of at most this many bricks pipeline prep/cull with integrate (a quarter of a
+// 512^3 grid: the shards of 4- and 8-GPU jobs; measured in DESIGN.md §6).
+constexpr long long kPipelineMaxBricks = 65536;
+
 // State common to the dense and hash handles.
 struct Base {
     int device = 0;
@@ -58,11 +62,24 @@ struct Base {
     Vol vol{};
     Pool pool{};
     long long n_bricks = 0;
+    // Per-batch buffers of the CURRENT buffer set (use_set): with the pipeline on, batches
+    // alternate between two sets so that prep + cull of batch k+1 can run while batch k integrates.
     float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
     unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
     int pyr_H = 0, pyr_W = 0;
     unsigned* list = nullptr;   // per-batch list of (brick | frame mask << 24) kept by the cull
     unsigned int* count = nullptr;
+    float* pyr_set[2] = {nullptr, nullptr};
+    unsigned* rgbx_set[2] = {nullptr, nullptr};
+    unsigned* list_set[2] = {nullptr, nullptr};
+    unsigned int* count_set[2] = {nullptr, nullptr};
+    unsigned short* dmask_set[2] = {nullptr, nullptr};
+    // Pipeline (dense handles, enable_pipeline): prep + cull on pstream, integrate on stream.
+    bool pipe = false;
+    hipStream_t pstream = nullptr;
+    hipEvent_t ev_culled[2] = {nullptr, nullptr};  // set's list complete (pstream)
+    hipEvent_t ev_done[2] = {nullptr, nullptr};    // set's last integrate finished (stream)
+    long long batches = 0;                         // batches issued since create (set = batches & 1)
     int n_cu = 256;             // compute units of the device
     PyrLayout lay{};
     unsigned long long* stats = nullptr;  // kNStat x kStatSpread
@@ -87,6 +104,16 @@ struct Base {
 
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
+    int enable_pipeline();
+    void use_set(int s) {
+        pyr = pyr_set[s];
+        rgbx = rgbx_set[s];
+        list = list_set[s];
+        count = count_set[s];
+        dmask = dmask_set[s];
+    }
+    hipStream_t prep_stream() const { return pipe ? pstream : stream; }
+    int sync_all();  // both compute streams (before reallocating per-batch buffers)
     int ensure_pyr(int H, int W);
     // Frame constants of frames [first, first+n) (n <= kMaxBatch) of a call, each with its own
     // per-frame buffers; host inputs are staged to the device when needed.
@@ -100,7 +127,7 @@ struct Base {
     int begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags);
     int end_batch(int flags);
     int end_call(int flags);
-    int launch_prep(const Batch& bt, int dk, int ck, int W, int H);
+    int launch_prep(const Batch& bt, int dk, int ck, int W, int H, hipStream_t st);
     // Workgroups of the integrate kernel: as many as can be resident (occupancy x CUs), capped
     // by the work there can be (4 bricks per workgroup per round).
     unsigned grid_for(const void* kernel);
