@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
 if [ $rc -eq 0 ] || [ $rc -eq 1 ]; then
