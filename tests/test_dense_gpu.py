@@ -316,10 +316,11 @@ def test_invalid_65535_mask_on_device(gf):
 
 @pytest.mark.parametrize("ingest", ["device", "host"])
 def test_prep_cull_pipeline_on_and_off_bit_identical(gf, monkeypatch, ingest):
-    """Small volumes pipeline prep + cull of batch k+1 with integrate k on a second stream and a
-    second buffer set (tsdf_dense.hip); large ones run them in line.  Both paths,
-    forced with TSDF_PIPELINE, over 29 async frames (4 batches, both sets reused) with 65535
-    masking, equal each other and the oracle bit for bit."""
+    """u16 + RGB8 calls run as three-stage pipeline launches (k_fused: integrate batch k, cull
+    k+1 and prep k+2 in one launch, three buffer sets, four staging slots; tsdf_dense.hip,
+    DESIGN.md §6); TSDF_PIPELINE=0 forces the in-line prep / cull / integrate kernels.  Both
+    paths over 29 async frames (4 batches: every set and slot reused) with 65535 masking, from
+    device and from host memory, equal each other and the oracle bit for bit."""
     import torch
     d, c, poses = _synth(29, start=11)
     d = np.ascontiguousarray(d).astype(np.uint16)

@@ -34,12 +34,22 @@ PyrLayout pyr_layout(int H, int W) {
     return l;
 }
 
+// Timing-only events: no system-scope fence when they complete (hip_runtime_api.h documents
+// hipEventDisableSystemFence for exactly this use), so recording them does not add a cache
+// writeback between the kernels they bracket.  TSDF_PROF_EVFLAGS overrides (A/B).
+static int new_timing_event(hipEvent_t* e) {
+    const char* ef = getenv("TSDF_PROF_EVFLAGS");
+    const unsigned fl = ef ? (unsigned)strtoul(ef, nullptr, 0) : (unsigned)hipEventDisableSystemFence;
+    TSDF_HIP(hipEventCreateWithFlags(e, fl));
+    return TSDF_OK;
+}
+
 int Profiler::begin(hipStream_t s, hipEvent_t* e0) {
     *e0 = nullptr;
     if (!on) return TSDF_OK;
     if (spare.empty()) {
         hipEvent_t e;
-        TSDF_HIP(hipEventCreate(&e));
+        TSDF_TRY(new_timing_event(&e));
         spare.push_back(e);
     }
     *e0 = spare.back();
@@ -52,7 +62,7 @@ int Profiler::end(hipStream_t s, hipEvent_t e0) {
     if (!on || !e0) return TSDF_OK;
     if (spare.empty()) {
         hipEvent_t e;
-        TSDF_HIP(hipEventCreate(&e));
+        TSDF_TRY(new_timing_event(&e));
         spare.push_back(e);
     }
     hipEvent_t e1 = spare.back();
@@ -128,10 +138,10 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     if (n_bricks >= (1ll << 24)) return set_error(TSDF_E_ARG, "too many bricks (%lld >= 2^24)", n_bricks);
     TSDF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     TSDF_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSlots; ++k) {
         TSDF_HIP(hipEventCreateWithFlags(&ev_copied[k], hipEventDisableTiming));
         TSDF_HIP(hipEventCreateWithFlags(&ev_free[k], hipEventDisableTiming));
-        TSDF_HIP(hipEventRecord(ev_free[k], stream));      // both slots start free
+        TSDF_HIP(hipEventRecord(ev_free[k], stream));      // every slot starts free
         TSDF_HIP(hipEventRecord(ev_copied[k], cstream));
     }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
@@ -148,61 +158,43 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     return TSDF_OK;
 }
 
-// Second buffer set + prep stream: prep and cull of batch k+1 overlap integrate k.  Pays off when
-// the integrate is short (a shard of a multi-GPU volume): there the fixed-latency prep/cull
-// would otherwise leave the GPU idle between integrates.  On a full volume the overlapping
-// kernels only take CUs from the integrate, so the caller decides.
-int Base::enable_pipeline() {
-    if (pipe) return TSDF_OK;
-    int least = 0, greatest = 0;
-    TSDF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    const char* pe = getenv("TSDF_PIPE_PRIO");
-    const int prio = pe ? atoi(pe) : 1;
-    if (prio >= 1) {  // prep/cull fill the CUs the integrate leaves (its tail) instead of sharing them
-        TSDF_HIP(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, least));
-    } else {
-        TSDF_HIP(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
+// Buffer sets 1..n-1 (lists and counters now; pyramids, RGBX and masks when a batch needs them).
+int Base::use_sets(int n) {
+    if (n <= n_sets) return TSDF_OK;
+    TSDF_TRY(sync_all());
+    for (int k = n_sets; k < n; ++k) {
+        TSDF_HIP(hipMalloc(&list_set[k], sizeof(unsigned) * (size_t)n_bricks));
+        TSDF_HIP(hipMalloc(&count_set[k], sizeof(unsigned int) * 4));
+        TSDF_HIP(hipMemsetAsync(count_set[k], 0, sizeof(unsigned int) * 4, stream));
     }
-    if (prio >= 2) {
-        TSDF_HIP(hipStreamDestroy(stream));
-        TSDF_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, greatest));
-    }
-    for (int k = 0; k < 2; ++k) {
-        TSDF_HIP(hipEventCreateWithFlags(&ev_culled[k], hipEventDisableTiming));
-        TSDF_HIP(hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming));
-        TSDF_HIP(hipEventRecord(ev_done[k], stream));
-    }
-    TSDF_HIP(hipMalloc(&list_set[1], sizeof(unsigned) * (size_t)n_bricks));
-    TSDF_HIP(hipMalloc(&count_set[1], sizeof(unsigned int) * 4));
-    TSDF_HIP(hipMemsetAsync(count_set[1], 0, sizeof(unsigned int) * 4, stream));
     TSDF_HIP(hipStreamSynchronize(stream));
-    pipe = true;
+    n_sets = n;
     return TSDF_OK;
 }
 
 int Base::sync_all() {
     TSDF_HIP(hipStreamSynchronize(stream));
-    if (pstream) TSDF_HIP(hipStreamSynchronize(pstream));
+    if (cstream) TSDF_HIP(hipStreamSynchronize(cstream));
     return TSDF_OK;
 }
 
 int Base::ensure_pyr(int H, int W) {
-    if (pyr_set[0] && H == pyr_H && W == pyr_W && (!pipe || pyr_set[1])) return TSDF_OK;
+    if (pyr_set[0] && H == pyr_H && W == pyr_W && pyr_set[n_sets - 1]) return TSDF_OK;
     TSDF_TRY(sync_all());
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSets; ++k) {
         if (pyr_set[k]) TSDF_HIP(hipFree(pyr_set[k]));
         if (rgbx_set[k]) TSDF_HIP(hipFree(rgbx_set[k]));
         pyr_set[k] = nullptr;
         rgbx_set[k] = nullptr;
     }
     lay = pyr_layout(H, W);
-    for (int k = 0; k < (pipe ? 2 : 1); ++k) {
+    for (int k = 0; k < n_sets; ++k) {
         TSDF_HIP(hipMalloc(&pyr_set[k], sizeof(float) * (size_t)lay.total * kMaxBatch));
         TSDF_HIP(hipMalloc(&rgbx_set[k], sizeof(unsigned) * (size_t)H * W * kMaxBatch));
     }
     pyr_H = H;
     pyr_W = W;
-    use_set(pipe ? (int)(batches & 1) : 0);
+    use_set(cur_set);
     return TSDF_OK;
 }
 
@@ -258,19 +250,18 @@ static void par_memcpy(void* dst, const void* src, size_t bytes) {
 
 int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
                         int W, const double K[9], const double* Tinv, const double* ow,
-                        double ow_default, int flags, int first, int n) {
+                        double ow_default, int flags, int first, int n, int slot) {
+    // the caller selected this batch's buffer set (use_set); reallocation keeps the selection
     TSDF_TRY(ensure_pyr(H, W));
     const size_t npx = (size_t)H * W;
     const size_t dbytes = npx * (dk == TSDF_DEPTH_U16_MM ? 2 : 8);
     const size_t cbytes = npx * (ck == TSDF_COLOR_RGB8 ? 3 : 4);
     const char* d = (const char*)depth + dbytes * (size_t)first;
     const char* c = (const char*)color + cbytes * (size_t)first;
-    if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames into slot call_batch & 1
-        const int slot = (int)(call_batch & 1);
+    if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames into staging slot `slot`
         if (st_depth_bytes < dbytes * kMaxBatch || st_color_bytes < cbytes * kMaxBatch) {
             TSDF_TRY(sync_all());
-            TSDF_HIP(hipStreamSynchronize(cstream));
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < kSlots; ++k) {
                 if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
                 if (st_color[k]) TSDF_HIP(hipFree(st_color[k]));
                 if (hst_depth[k]) TSDF_HIP(hipHostFree(hst_depth[k]));
@@ -278,7 +269,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
                 st_depth[k] = st_color[k] = hst_depth[k] = hst_color[k] = nullptr;
             }
             st_depth_bytes = st_color_bytes = 0;
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < kSlots; ++k) {
                 TSDF_HIP(hipMalloc(&st_depth[k], dbytes * kMaxBatch));
                 TSDF_HIP(hipMalloc(&st_color[k], cbytes * kMaxBatch));
                 TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * kMaxBatch, hipHostMallocDefault));
@@ -295,23 +286,22 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         TSDF_HIP(hipMemcpyAsync(st_depth[slot], hst_depth[slot], dbytes * n, hipMemcpyHostToDevice, cstream));
         TSDF_HIP(hipMemcpyAsync(st_color[slot], hst_color[slot], cbytes * n, hipMemcpyHostToDevice, cstream));
         TSDF_HIP(hipEventRecord(ev_copied[slot], cstream));
-        TSDF_HIP(hipStreamWaitEvent(prep_stream(), ev_copied[slot], 0));
-        if (pipe) TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
+        TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
         d = (const char*)st_depth[slot];
         c = (const char*)st_color[slot];
     }
     const bool mask = (flags & TSDF_DEPTH_INVALID_65535) && dk == TSDF_DEPTH_U16_MM;
-    if (mask && (dmask_px < npx || (pipe && !dmask_set[1]))) {
+    if (mask && (dmask_px < npx || !dmask_set[n_sets - 1])) {
         TSDF_TRY(sync_all());
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kSets; ++k) {
             if (dmask_set[k]) TSDF_HIP(hipFree(dmask_set[k]));
             dmask_set[k] = nullptr;
         }
-        for (int k = 0; k < (pipe ? 2 : 1); ++k)
+        for (int k = 0; k < n_sets; ++k)
             TSDF_HIP(hipMalloc(&dmask_set[k], sizeof(unsigned short) * npx * kMaxBatch));
         dmask_px = npx;
-        use_set(pipe ? (int)(batches & 1) : 0);
     }
+    use_set(cur_set);  // (re)read the set's pointers: the buffers above may be new
     bt->n = n;
     for (int i = 0; i < n; ++i) {
         Frame* fr = &bt->f[i];
@@ -344,13 +334,11 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
 
 int Base::begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags) {
     (void)depth, (void)dbytes, (void)color, (void)cbytes, (void)flags;
-    call_batch = 0;
     return TSDF_OK;
 }
 
-int Base::end_batch(int flags) {
-    if (!(flags & TSDF_DEVICE_PTRS)) TSDF_HIP(hipEventRecord(ev_free[call_batch & 1], stream));
-    ++call_batch;
+int Base::end_batch(int flags, int slot) {
+    if (!(flags & TSDF_DEVICE_PTRS)) TSDF_HIP(hipEventRecord(ev_free[slot], stream));
     return TSDF_OK;
 }
 
@@ -379,12 +367,12 @@ int Base::launch_prep(const Batch& bt, int dk, int ck, int W, int H, hipStream_t
     return TSDF_OK;
 }
 
-unsigned Base::grid_for(const void* kernel) {
+unsigned Base::grid_for(const void* kernel, int wg) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWG, 0) != hipSuccess || per_cu < 1)
-        per_cu = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1024 / wg;
     long long g = (long long)per_cu * n_cu;
-    const long long need = (n_bricks + (kWG / 64) - 1) / (kWG / 64);
+    const long long need = (n_bricks + (wg / 64) - 1) / (wg / 64);
     if (g > need) g = need;
     return (unsigned)(g < 1 ? 1 : g);
 }
@@ -434,31 +422,25 @@ int Base::set_profiling(int on) {
 
 void Base::release() {
     if (stream) (void)hipStreamSynchronize(stream);
-    if (pstream) (void)hipStreamSynchronize(pstream);
     prof.release();
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSets; ++k) {
         if (pyr_set[k]) (void)hipFree(pyr_set[k]);
         if (rgbx_set[k]) (void)hipFree(rgbx_set[k]);
         if (list_set[k]) (void)hipFree(list_set[k]);
         if (count_set[k]) (void)hipFree(count_set[k]);
         if (dmask_set[k]) (void)hipFree(dmask_set[k]);
-        if (ev_culled[k]) (void)hipEventDestroy(ev_culled[k]);
-        if (ev_done[k]) (void)hipEventDestroy(ev_done[k]);
         pyr_set[k] = nullptr;
         rgbx_set[k] = nullptr;
         list_set[k] = nullptr;
         count_set[k] = nullptr;
         dmask_set[k] = nullptr;
-        ev_culled[k] = ev_done[k] = nullptr;
     }
-    if (pstream) (void)hipStreamDestroy(pstream);
-    pstream = nullptr;
-    pipe = false;
+    n_sets = 1;
     if (rcp) (void)hipFree(rcp);
     rcp = nullptr;
     if (stats) (void)hipFree(stats);
     if (cstream) (void)hipStreamSynchronize(cstream);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSlots; ++k) {
         if (st_depth[k]) (void)hipFree(st_depth[k]);
         if (st_color[k]) (void)hipFree(st_color[k]);
         if (ev_copied[k]) (void)hipEventDestroy(ev_copied[k]);
@@ -467,7 +449,7 @@ void Base::release() {
         ev_copied[k] = ev_free[k] = nullptr;
     }
     dmask = nullptr;
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSlots; ++k) {
         if (hst_depth[k]) (void)hipHostFree(hst_depth[k]);
         if (hst_color[k]) (void)hipHostFree(hst_color[k]);
         hst_depth[k] = hst_color[k] = nullptr;

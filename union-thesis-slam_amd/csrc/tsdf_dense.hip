@@ -12,6 +12,7 @@ struct tsdf_dense {
     Base b;
     Mesh mesh;
     int nz = 4;  // z-steps per wave in k_integrate (8: a brick per wave; 4: a z-half per wave)
+    bool fused = true;  // three-stage pipeline launches (k_fused) when a call allows them
 };
 
 namespace {
@@ -42,34 +43,25 @@ __global__ void k_relayout(Vol v, const float* __restrict__ src, float* __restri
     }
 }
 
-int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void* color, int ck,
-              int H, int W, const double* K, const double* Tinv, const double* ow, int flags) {
+// The in-line path: per batch prep, cull and integrate, one after the other on the handle's
+// stream.  Serves every input format.
+int dense_run_inline(tsdf_dense* h, int n_frames, const void* depth, int dk, const void* color, int ck,
+                     int H, int W, const double* K, const double* Tinv, const double* ow, int flags) {
     Base& B = h->b;
-    TSDF_HIP(hipSetDevice(B.device));
     const Table no_table{};
     const unsigned cull_grid = B.cull_grid();
     const unsigned grid = h->nz == 4 ? 2 * B.grid_for((const void*)k_integrate<false, 0, 0, true, 4>)
                                      : B.grid_for((const void*)k_integrate<false, 0, 0, true, 8>);
-    TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
-                          frame_bytes_color(ck, H, W) * n_frames, flags));
-    CallGuard guard(B, flags);
+    B.use_set(0);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
-        const int set = B.pipe ? (int)(B.batches & 1) : 0;
-        B.use_set(set);
-        TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, ow, 1.0, flags, f0, n));
-        const hipStream_t ps = B.prep_stream();
-        // pipelined: the set's previous integrate (batch k-2) must be done before prep overwrites it
-        if (B.pipe) TSDF_HIP(hipStreamWaitEvent(ps, B.ev_done[set], 0));
-        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, ps));
-        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kCullWG), 0, ps, B.vol, bt, no_table,
+        const int slot = (f0 / kMaxBatch) % kSlots;
+        TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, ow, 1.0, flags, f0, n, slot));
+        TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, B.stream));
+        hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, no_table,
                            B.list, B.count, B.stats);
         TSDF_HIP(hipGetLastError());
-        if (B.pipe) {
-            TSDF_HIP(hipEventRecord(B.ev_culled[set], ps));
-            TSDF_HIP(hipStreamWaitEvent(B.stream, B.ev_culled[set], 0));
-        }
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
         bool ow1 = true;
@@ -103,11 +95,95 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
         }
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
-        if (B.pipe) TSDF_HIP(hipEventRecord(B.ev_done[set], B.stream));
-        TSDF_TRY(B.end_batch(flags));
+        TSDF_TRY(B.end_batch(flags, slot));
         B.frames += n;
-        ++B.batches;
     }
+    return TSDF_OK;
+}
+
+// The fused path (k_fused, tsdf_device.h): launch L runs integrate(L), cull(L+1) and prep(L+2)
+// of the call's batches, L = -2 .. nb-1.  Batch j uses buffer set and staging slot j % kSets.
+// u16 depth + RGB8 with the vectorised prep's alignment only (the bench's and the demos' case).
+int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, const void* color, int H, int W,
+                    const double* K, const double* Tinv, const double* ow, int flags) {
+    Base& B = h->b;
+    TSDF_TRY(B.use_sets(kSets));
+    const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
+    const int gi_full = h->nz == 4 ? (int)B.grid_for((const void*)k_fused<true, 4>, kFusedWG)
+                                   : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
+    const int gc_full = (int)B.cull_grid();
+    Batch bts[kSets];
+    for (int L = -2; L < nb; ++L) {
+        const int jp = L + 2;  // batch prepped by this launch
+        if (jp < nb) {
+            const int f0 = jp * kMaxBatch;
+            const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+            B.use_set(jp % kSets);
+            TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, TSDF_DEPTH_U16_MM, color, TSDF_COLOR_RGB8, H, W,
+                                     K, Tinv, ow, 1.0, flags, f0, n, jp % kSlots));
+        }
+        const bool has_i = L >= 0, has_c = L + 1 >= 0 && L + 1 < nb, has_p = jp < nb;
+        static const Batch kNone{};
+        const Batch& bi = has_i ? bts[L % kSets] : kNone;
+        const Batch& bc = has_c ? bts[(L + 1) % kSets] : kNone;
+        const Batch& bp = has_p ? bts[jp % kSets] : kNone;
+        Stage sg{};
+        sg.gi = has_i ? gi_full : 0;
+        sg.gc = has_c ? gc_full : 0;
+        sg.ptx = (W + 63) / 64;
+        sg.pty = (H + 63) / 64;
+        if (has_i) {
+            sg.list_i = B.list_set[L % kSets];
+            sg.count_i = B.count_set[L % kSets];
+        }
+        if (has_c) {
+            sg.list_c = B.list_set[(L + 1) % kSets];
+            sg.count_c = B.count_set[(L + 1) % kSets];
+        }
+        if (has_p) sg.count_p = B.count_set[jp % kSets];
+        const long long grid = (long long)sg.gi + sg.gc + (has_p ? (long long)sg.ptx * sg.pty * bp.n : 0);
+        if (grid >= (1ll << 31)) return set_error(TSDF_E_ARG, "fused grid too large");
+        bool ow1 = true;
+        for (int i = 0; i < bi.n; ++i) ow1 = ow1 && bi.f[i].ow == 1.0;
+        hipEvent_t e0 = nullptr;
+        if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
+        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0);
+        switch (sel) {
+#define TSDF_LAUNCH(S, OW_, NZ_)                                                                        \
+    case S:                                                                                             \
+        hipLaunchKernelGGL((k_fused<OW_, NZ_>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, \
+                           bc, bp, B.pool, B.stats, sg);                                                \
+        break;
+            TSDF_LAUNCH(0, false, 8)
+            TSDF_LAUNCH(1, true, 8)
+            TSDF_LAUNCH(2, false, 4)
+            TSDF_LAUNCH(3, true, 4)
+#undef TSDF_LAUNCH
+        }
+        TSDF_HIP(hipGetLastError());
+        if (has_i) {
+            TSDF_TRY(B.prof.end(B.stream, e0));
+            TSDF_TRY(B.end_batch(flags, L % kSlots));  // batch L's frames: last read by this launch
+            B.frames += bi.n;
+        }
+    }
+    return TSDF_OK;
+}
+
+int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void* color, int ck,
+              int H, int W, const double* K, const double* Tinv, const double* ow, int flags) {
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
+                          frame_bytes_color(ck, H, W) * n_frames, flags));
+    CallGuard guard(B, flags);
+    // the fused pipeline needs the vectorised prep: u16 + RGB8, W % 4 == 0 and (device frames)
+    // 8-byte depth / 4-byte colour alignment of every frame (host frames are staged aligned)
+    bool fused = h->fused && dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
+    if (fused && (flags & TSDF_DEVICE_PTRS))
+        fused = (uintptr_t)depth % 8 == 0 && (uintptr_t)color % 4 == 0 && ((size_t)H * W) % 4 == 0;
+    if (fused) TSDF_TRY(dense_run_fused(h, n_frames, depth, color, H, W, K, Tinv, ow, flags));
+    else TSDF_TRY(dense_run_inline(h, n_frames, depth, dk, color, ck, H, W, K, Tinv, ow, flags));
     TSDF_TRY(guard.finish());
     if (!(flags & TSDF_ASYNC)) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;
@@ -163,11 +239,8 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
         if (gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
     }
     if (r == TSDF_OK) {
-        // prep/cull pipeline: on for small volumes (the integrate is then short),
-        // TSDF_PIPELINE=0/1 overrides
-        bool pipe = h->b.n_bricks <= kPipelineMaxBricks;
-        if (const char* e = getenv("TSDF_PIPELINE")) pipe = atoi(e) != 0;
-        if (pipe) r = h->b.enable_pipeline();
+        // three-stage pipeline launches; TSDF_PIPELINE=0 forces the in-line path
+        if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;
     }
     if (r == TSDF_OK) {
         const size_t n = (size_t)h->b.n_bricks * kBrickVox * sizeof(float);

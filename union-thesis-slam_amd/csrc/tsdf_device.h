@@ -724,10 +724,9 @@ constexpr int kCullWG = 64 * kMaxBatch;  // k_cull: one wave per frame of the ba
 // wave 0 appends the kept bricks to the list (one atomicAdd per superbrick with survivors).
 // Every test is at most two cull_brick latencies deep, whatever the batch size.
 template <bool HASH>
-__global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, unsigned* list,
-                                                  unsigned int* count, unsigned long long* stats) {
-    __shared__ unsigned s_mask[64];
-    __shared__ unsigned long long s_stat[kNStat];
+__device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Table& tab, unsigned* list,
+                                       unsigned int* count, unsigned long long* stats, int si,
+                                       unsigned* s_mask, unsigned long long* s_stat) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int f = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid < 64) s_mask[tid] = 0u;
@@ -735,7 +734,6 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, un
     __syncthreads();
     const int nsy = (v.nb[1] + (1 << v.sb[1]) - 1) >> v.sb[1];
     const int nsz = (v.nb[2] + (1 << v.sb[2]) - 1) >> v.sb[2];
-    const int si = blockIdx.x;
     const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
     const int ex = 1 << v.sb[0], ey = 1 << v.sb[1], ez = 1 << v.sb[2];
     const int lz = lane & (ez - 1), ly = (lane >> v.sb[2]) & (ey - 1), lx = lane >> (v.sb[1] + v.sb[2]);
@@ -771,10 +769,29 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, un
     flush_stats(s_stat, stats);
 }
 
+template <bool HASH>
+__global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, unsigned* list,
+                                                  unsigned int* count, unsigned long long* stats) {
+    __shared__ unsigned s_mask[64];
+    __shared__ unsigned long long s_stat[kNStat];
+    cull_superbrick<HASH>(v, bt, tab, list, count, stats, blockIdx.x, s_mask, s_stat);
+}
+
 // Integrate the listed bricks: each wave takes list entries gw, gw + NW, ... (NW = waves in the
 // grid, all resident), so the work is spread evenly whatever the frames see.  `count` (device)
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
+template <bool HASH, int DK, int CK, bool OW1, int NZ>
+__device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
+                                      const unsigned* list, unsigned int* count, int n_list, int wave,
+                                      int n_waves, unsigned long long* s_stat, const double* s_rcp) {
+    constexpr int parts = 8 / NZ;  // waves per listed brick
+    const int n = (count ? (int)coh_load(count) : n_list) * parts;
+    for (int e = wave; e < n; e += n_waves)
+        integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
+                                               s_stat, s_rcp);
+}
+
 template <bool HASH, int DK, int CK, bool OW1, int NZ = 8>
 #ifndef TSDF_INTEGRATE_ATTR
 #define TSDF_INTEGRATE_ATTR __attribute__((amdgpu_waves_per_eu(4)))  // <= 128 VGPRs: 4 waves/SIMD
@@ -789,12 +806,9 @@ __global__ __launch_bounds__(kWG) TSDF_INTEGRATE_ATTR void k_integrate(Vol v, Ba
     if (OW1)  // 32 KB table copied with 16-byte loads (computing it cost 16 f64 divisions per thread)
         for (int i = tid; i < kRcpTab / 2; i += kWG) ((double2*)s_rcp)[i] = ((const double2*)v.rcp)[i];
     __syncthreads();
-    constexpr int parts = 8 / NZ;  // waves per listed brick
-    const int n = (count ? (int)coh_load(count) : n_list) * parts;
-    const int nw = gridDim.x * (kWG / 64);
-    for (int e = blockIdx.x * (kWG / 64) + (tid >> 6); e < n; e += nw)
-        integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
-                                               s_stat, OW1 ? s_rcp : nullptr);
+    integrate_list<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list, count, n_list,
+                                          blockIdx.x * (kWG / 64) + (tid >> 6), gridDim.x * (kWG / 64),
+                                          s_stat, OW1 ? s_rcp : nullptr);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
@@ -805,14 +819,14 @@ __global__ __launch_bounds__(kWG) TSDF_INTEGRATE_ATTR void k_integrate(Vol v, Ba
 // brick-list counter.  One 1024-thread workgroup per 64x64 tile, 2x2 pixels per thread.
 template <int REDUCE>
 __device__ inline void pyr_level(const Frame& fr, float* pyr, int L, const float (*src)[33],
-                                 float (*dst)[33], int n) {
+                                 float (*dst)[33], int n, int tx = blockIdx.x, int ty = blockIdx.y) {
     const int t = threadIdx.x;
     if (t < n * n) {
         const int rr = t / n, cc = t - rr * n;
         const float m = fmaxf(fmaxf(src[2 * rr][2 * cc], src[2 * rr][2 * cc + 1]),
                               fmaxf(src[2 * rr + 1][2 * cc], src[2 * rr + 1][2 * cc + 1]));
         dst[rr][cc] = m;
-        const int X = blockIdx.x * n + cc, Y = blockIdx.y * n + rr;
+        const int X = tx * n + cc, Y = ty * n + rr;
         if (X < fr.pyr_w[L] && Y < fr.pyr_h[L]) pyr[fr.pyr_off[L] + Y * fr.pyr_w[L] + X] = m;
     }
 }
@@ -821,15 +835,13 @@ __device__ inline void pyr_level(const Frame& fr, float* pyr, int L, const float
 // per 64x64 tile, 4x2 pixels per thread, moved with 8-byte depth loads, three 4-byte colour loads
 // per row (4 packed RGB pixels) and one 16-byte RGBX store per row -- instead of one 2-byte and
 // three 1-byte loads and one 4-byte store per pixel.  Same outputs as k_prep<0, 0>.
-template <int = 0>
-__global__ __launch_bounds__(512) void k_prep_vec(Batch bt, unsigned int* count) {
-    __shared__ float sa[32][33];
-    __shared__ float sb[32][33];
-    const Frame& fr = bt.f[blockIdx.z];
+__device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int tx, int ty, int tf,
+                                     float (*sa)[33], float (*sb)[33]) {
+    const Frame& fr = bt.f[tf];
     float* pyr = (float*)fr.pyr;
     const int t = threadIdx.x, r = t >> 4, c = t & 15;
-    if (count && t == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count, 0u);
-    const int x0 = blockIdx.x * 64 + c * 4, y0 = blockIdx.y * 64 + r * 2;
+    if (count && t == 0 && tx == 0 && ty == 0 && tf == 0) coh_store(count, 0u);
+    const int x0 = tx * 64 + c * 4, y0 = ty * 64 + r * 2;
     float ma = 0.0f, mb = 0.0f;  // level-1 texels (x0/2, y0/2) and (x0/2 + 1, y0/2)
     if (x0 < fr.W) {
 #pragma unroll
@@ -865,15 +877,22 @@ __global__ __launch_bounds__(512) void k_prep_vec(Batch bt, unsigned int* count)
     sa[r][2 * c] = ma;
     sa[r][2 * c + 1] = mb;
     __syncthreads();
-    pyr_level<0>(fr, pyr, 2, sa, sb, 16);
+    pyr_level<0>(fr, pyr, 2, sa, sb, 16, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 3, sb, sa, 8);
+    pyr_level<0>(fr, pyr, 3, sb, sa, 8, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 4, sa, sb, 4);
+    pyr_level<0>(fr, pyr, 4, sa, sb, 4, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 5, sb, sa, 2);
+    pyr_level<0>(fr, pyr, 5, sb, sa, 2, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 6, sa, sb, 1);
+    pyr_level<0>(fr, pyr, 6, sa, sb, 1, tx, ty);
+}
+
+template <int = 0>
+__global__ __launch_bounds__(512) void k_prep_vec(Batch bt, unsigned int* count) {
+    __shared__ float sa[32][33];
+    __shared__ float sb[32][33];
+    prep_vec_tile(bt, count, blockIdx.x, blockIdx.y, blockIdx.z, sa, sb);
 }
 
 template <int DK, int CK>
@@ -927,6 +946,59 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
     pyr_level<0>(fr, pyr, 5, sb, sa, 2);
     __syncthreads();
     pyr_level<0>(fr, pyr, 6, sa, sb, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// One launch of the dense grid's three-stage software pipeline.  Launch k runs
+//   workgroups [0, gi)          integrate batch k   (list set k, written by launch k-1),
+//   workgroups [gi, gi + gc)    cull batch k+1      (one superbrick each; pyramid of launch k-1),
+//   the rest                    prep batch k+2      (one 64x64 tile of one frame each).
+// The stages touch disjoint buffer sets (batch j uses set j % 3) and every input of a stage was
+// written by an earlier launch on the same stream, so no workgroup ever waits for another.  The
+// integrate workgroups come first in dispatch order; the cull and prep workgroups take the CUs
+// its tail frees.  One launch per batch replaces three kernels and the gaps between them.
+// ---------------------------------------------------------------------------------------------
+constexpr int kFusedWG = 512;
+static_assert(kFusedWG == kCullWG, "a cull workgroup is one wave per frame of the batch");
+struct Stage {
+    const unsigned* list_i;  // integrate: list and count of batch k
+    unsigned int* count_i;
+    unsigned* list_c;        // cull: list and count of batch k+1
+    unsigned int* count_c;
+    unsigned int* count_p;   // prep: count of batch k+2 (reset for its cull)
+    int gi, gc;              // integrate / cull workgroups
+    int ptx, pty;            // prep tiles per frame (x, y)
+};
+
+template <bool OW1, int NZ>
+__global__ __launch_bounds__(kFusedWG) TSDF_INTEGRATE_ATTR void k_fused(Vol v, Batch bi, Batch bc, Batch bp,
+                                                                     Pool pool, unsigned long long* stats,
+                                                                     Stage sg) {
+    // integrate: RN(1/n) table; cull: per-brick frame masks; prep: two pyramid tiles
+    __shared__ double s_buf[kRcpTab];
+    __shared__ unsigned long long s_stat[kNStat];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const Table no_table{};
+    if (b < sg.gi) {
+        if (tid < kNStat) s_stat[tid] = 0;
+        if (OW1)
+            for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
+        __syncthreads();
+        constexpr int wpg = kFusedWG / 64;
+        integrate_list<false, 0, 0, OW1, NZ>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
+                                             b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
+                                             OW1 ? s_buf : nullptr);
+        __syncthreads();
+        flush_stats(s_stat, stats);
+    } else if (b < sg.gi + sg.gc) {
+        cull_superbrick<false>(v, bc, no_table, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
+                               s_stat);
+    } else {
+        const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
+        const int f = t / per, r = t - f * per;
+        float(*sa)[33] = (float(*)[33])s_buf;
+        prep_vec_tile(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
+    }
 }
 
 }  // namespace tsdf

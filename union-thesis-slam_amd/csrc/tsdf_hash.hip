@@ -388,8 +388,9 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+        const int slot = (f0 / kMaxBatch) % kSlots;
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
-        TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, nullptr, 1.0, flags, f0, n));
+        TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, nullptr, 1.0, flags, f0, n, slot));
         TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, B.stream));
         hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, h->t, B.list,
                            B.count, B.stats);
@@ -403,7 +404,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         TSDF_HIP(hipGetLastError());
         B.frames += n;
         if (!sync) {
-            TSDF_TRY(B.end_batch(flags));
+            TSDF_TRY(B.end_batch(flags, slot));
             continue;
         }
         // Synchronous: recover from a full table/pool exactly (the skipped bricks were not
@@ -431,7 +432,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
             TSDF_TRY(read_state(h));
         }
         if (h->host_st.n_overflow > 0) return set_error(TSDF_E_CAPACITY, "could not make room in the hash table");
-        TSDF_TRY(B.end_batch(flags));  // the overflow re-runs above read this batch's frames
+        TSDF_TRY(B.end_batch(flags, slot));  // the overflow re-runs above read this batch's frames
         TSDF_TRY(ensure_room(h));
     }
     TSDF_TRY(guard.finish());

@@ -51,9 +51,12 @@ struct Profiler {
     void release();
 };
 
-// Dense handles of at most this many bricks pipeline prep/cull with integrate (a quarter of a
-// 512^3 grid: the shards of 4- and 8-GPU jobs; measured in DESIGN.md §6).
-constexpr long long kPipelineMaxBricks = 65536;
+// Buffer sets: batch j of a call uses set j % kSets (the fused dense pipeline has batches k,
+// k+1 and k+2 in flight in one launch; the in-line path only ever uses set 0).  Host-pointer
+// frames of batch j are staged in slot j % kSlots and stay there until the launch that
+// integrates them ends; the fourth slot lets the DMA of batch k+2 overlap launch k-1.
+constexpr int kSets = 3;
+constexpr int kSlots = 4;
 
 // State common to the dense and hash handles.
 struct Base {
@@ -62,24 +65,18 @@ struct Base {
     Vol vol{};
     Pool pool{};
     long long n_bricks = 0;
-    // Per-batch buffers of the CURRENT buffer set (use_set): with the pipeline on, batches
-    // alternate between two sets so that prep + cull of batch k+1 can run while batch k integrates.
+    // Per-batch buffers of the CURRENT buffer set (use_set).
     float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
     unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
     int pyr_H = 0, pyr_W = 0;
     unsigned* list = nullptr;   // per-batch list of (brick | frame mask << 24) kept by the cull
     unsigned int* count = nullptr;
-    float* pyr_set[2] = {nullptr, nullptr};
-    unsigned* rgbx_set[2] = {nullptr, nullptr};
-    unsigned* list_set[2] = {nullptr, nullptr};
-    unsigned int* count_set[2] = {nullptr, nullptr};
-    unsigned short* dmask_set[2] = {nullptr, nullptr};
-    // Pipeline (dense handles, enable_pipeline): prep + cull on pstream, integrate on stream.
-    bool pipe = false;
-    hipStream_t pstream = nullptr;
-    hipEvent_t ev_culled[2] = {nullptr, nullptr};  // set's list complete (pstream)
-    hipEvent_t ev_done[2] = {nullptr, nullptr};    // set's last integrate finished (stream)
-    long long batches = 0;                         // batches issued since create (set = batches & 1)
+    float* pyr_set[kSets] = {};
+    unsigned* rgbx_set[kSets] = {};
+    unsigned* list_set[kSets] = {};
+    unsigned int* count_set[kSets] = {};
+    unsigned short* dmask_set[kSets] = {};
+    int n_sets = 1;             // buffer sets allocated (kSets once the fused pipeline is used)
     int n_cu = 256;             // compute units of the device
     PyrLayout lay{};
     unsigned long long* stats = nullptr;  // kNStat x kStatSpread
@@ -87,50 +84,51 @@ struct Base {
     long long frames = 0;
     Profiler prof;
     // Host-pointer frames (frame ingest): the host copies each batch (with
-    // several threads) into one of two page-locked bounce slots, a copy stream DMAs it into the
-    // matching device staging slot, and the compute stream integrates it -- while the host
-    // already fills the other slot.
+    // several threads) into one of kSlots page-locked bounce slots, a copy stream DMAs it into
+    // the matching device staging slot, and the compute stream integrates it -- while the host
+    // already fills the next slot.
     hipStream_t cstream = nullptr;
-    hipEvent_t ev_copied[2] = {nullptr, nullptr};  // slot's frames landed (copy stream)
-    hipEvent_t ev_free[2] = {nullptr, nullptr};    // slot's last reader finished (compute stream)
-    void* st_depth[2] = {nullptr, nullptr};
-    void* st_color[2] = {nullptr, nullptr};
+    hipEvent_t ev_copied[kSlots] = {};  // slot's frames landed (copy stream)
+    hipEvent_t ev_free[kSlots] = {};    // slot's last reader finished (compute stream)
+    void* st_depth[kSlots] = {};
+    void* st_color[kSlots] = {};
     size_t st_depth_bytes = 0, st_color_bytes = 0;
     unsigned short* dmask = nullptr;  // kMaxBatch masked u16 depth images (TSDF_DEPTH_INVALID_65535)
     size_t dmask_px = 0;
-    long long call_batch = 0;         // batches issued in the current call
-    void* hst_depth[2] = {nullptr, nullptr};  // page-locked bounce slots (hipHostMalloc)
-    void* hst_color[2] = {nullptr, nullptr};
+    void* hst_depth[kSlots] = {};      // page-locked bounce slots (hipHostMalloc)
+    void* hst_color[kSlots] = {};
 
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
-    int enable_pipeline();
+    int use_sets(int n);  // allocate n buffer sets (1 or kSets)
+    int cur_set = 0;
     void use_set(int s) {
+        cur_set = s;
         pyr = pyr_set[s];
         rgbx = rgbx_set[s];
         list = list_set[s];
         count = count_set[s];
         dmask = dmask_set[s];
     }
-    hipStream_t prep_stream() const { return pipe ? pstream : stream; }
-    int sync_all();  // both compute streams (before reallocating per-batch buffers)
+    int sync_all();  // compute and copy streams (before reallocating per-batch buffers)
     int ensure_pyr(int H, int W);
-    // Frame constants of frames [first, first+n) (n <= kMaxBatch) of a call, each with its own
-    // per-frame buffers; host inputs are staged to the device when needed.
+    // Frame constants of frames [first, first+n) (n <= kMaxBatch) of a call, with the per-frame
+    // buffers of the current set; host inputs are staged to the device through staging slot
+    // `slot` (the work that reads them must follow on `stream`).
     int prepare_batch(Batch* bt, const void* depth, int dk, const void* color, int ck, int H,
                       int W, const double K[9], const double* Tinv, const double* ow,
-                      double ow_default, int flags, int first, int n);
-    // Around the batches of one integrate call: end_batch marks the batch's staging slot
-    // reusable once the compute stream has finished with it.  begin_call / end_call bracket the
+                      double ow_default, int flags, int first, int n, int slot);
+    // Around the batches of one integrate call: end_batch marks staging slot `slot` reusable
+    // once the work issued so far on `stream` has finished.  begin_call / end_call bracket the
     // call (the caller's host arrays are read synchronously into the bounce slots, so nothing
     // of them is held past the call).
     int begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags);
-    int end_batch(int flags);
+    int end_batch(int flags, int slot);
     int end_call(int flags);
     int launch_prep(const Batch& bt, int dk, int ck, int W, int H, hipStream_t st);
     // Workgroups of the integrate kernel: as many as can be resident (occupancy x CUs), capped
-    // by the work there can be (4 bricks per workgroup per round).
-    unsigned grid_for(const void* kernel);
+    // by the work there can be (one brick per wave per round).
+    unsigned grid_for(const void* kernel, int wg = kWG);
     // Workgroups of k_cull: one per superbrick (Vol::sb).
     unsigned cull_grid() const {
         long long n = 1;
