@@ -145,9 +145,9 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
         TSDF_HIP(hipEventRecord(ev_copied[k], cstream));
     }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    TSDF_HIP(hipMalloc(&list_set[0], sizeof(unsigned) * (size_t)n_bricks));
-    TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * 4));
-    TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * 4, stream));
+    TSDF_HIP(hipMalloc(&list_set[0], sizeof(unsigned) * (size_t)n_bricks * kMaxBatch));
+    TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
+    TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * kCountWords, stream));
     use_set(0);
     TSDF_HIP(hipMalloc(&rcp, sizeof(double) * kRcpTab));
     hipLaunchKernelGGL(k_fill_rcp, dim3((kRcpTab + 255) / 256), dim3(256), 0, stream, rcp);
@@ -163,9 +163,9 @@ int Base::use_sets(int n) {
     if (n <= n_sets) return TSDF_OK;
     TSDF_TRY(sync_all());
     for (int k = n_sets; k < n; ++k) {
-        TSDF_HIP(hipMalloc(&list_set[k], sizeof(unsigned) * (size_t)n_bricks));
-        TSDF_HIP(hipMalloc(&count_set[k], sizeof(unsigned int) * 4));
-        TSDF_HIP(hipMemsetAsync(count_set[k], 0, sizeof(unsigned int) * 4, stream));
+        TSDF_HIP(hipMalloc(&list_set[k], sizeof(unsigned) * (size_t)n_bricks * kMaxBatch));
+        TSDF_HIP(hipMalloc(&count_set[k], sizeof(unsigned int) * kCountWords));
+        TSDF_HIP(hipMemsetAsync(count_set[k], 0, sizeof(unsigned int) * kCountWords, stream));
     }
     TSDF_HIP(hipStreamSynchronize(stream));
     n_sets = n;

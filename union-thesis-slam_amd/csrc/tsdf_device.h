@@ -751,18 +751,24 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         }
     }
     __syncthreads();
-    if (tid < 64) {
+    if (tid < 64) {  // append the kept bricks to the sub-list of their cost class (frames kept)
         const unsigned fmask = s_mask[lane];
-        const unsigned long long m = __ballot(fmask != 0u);
-        if (m) {
-            unsigned base = 0;
-            if (lane == 0) {
-                base = atomicAdd(count, (unsigned)__popcll(m));
-                s_stat[ST_VISITED] = (unsigned long long)__popcll(m);
+        const int cls = __popc(fmask);
+        const unsigned long long any = __ballot(cls != 0);
+        if (any) {
+            unsigned n_cls = 0, rank = 0;
+#pragma unroll
+            for (int c = 1; c <= kMaxBatch; ++c) {
+                const unsigned long long m = __ballot(cls == c);
+                if (lane == c) n_cls = (unsigned)__popcll(m);
+                if (cls == c) rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
             }
-            base = __shfl(base, 0);
-            const unsigned idx = base + __popcll(m & ((1ull << lane) - 1ull));
-            if (fmask && idx < (unsigned)(v.nb[0] * v.nb[1] * v.nb[2])) list[idx] = e | (fmask << 24);
+            unsigned base = 0;  // lanes 1..8 reserve their class's slots at once
+            if (lane >= 1 && lane <= kMaxBatch && n_cls) base = atomicAdd(&count[lane], n_cls);
+            if (lane == 0) s_stat[ST_VISITED] = (unsigned long long)__popcll(any);
+            base = __shfl(base, cls);
+            const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
+            if (cls && base + rank < nbk) list[(size_t)(cls - 1) * nbk + base + rank] = e | (fmask << 24);
         }
     }
     __syncthreads();
@@ -786,10 +792,32 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
                                       const unsigned* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
-    const int n = (count ? (int)coh_load(count) : n_list) * parts;
-    for (int e = wave; e < n; e += n_waves)
-        integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
-                                               s_stat, s_rcp);
+    wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
+    if (!count) {  // a flat list of n_list entries (hash overflow re-run)
+        for (int e = wave; e < n_list * parts; e += n_waves)
+            integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
+                                                   s_stat, s_rcp);
+        return;
+    }
+    // k_cull's list: one sub-list per cost class (frames kept, 1..kMaxBatch), taken most frames
+    // first, so that the round-robin hands every wave a similar amount of work (the longest-job-
+    // first order of list scheduling)
+    const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
+    unsigned ncls[kMaxBatch];
+    int total = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxBatch; ++c) {
+        ncls[c] = min(coh_load(&count[c + 1]), nbk);
+        total += (int)ncls[c];
+    }
+    int c = kMaxBatch - 1;
+    unsigned k0 = 0;  // list ordinal where class c starts (classes visited in descending order)
+    for (int e = wave; e < total * parts; e += n_waves) {
+        const unsigned k = (unsigned)(e / parts);
+        while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
+        integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
+                                               (e % parts) * NZ, s_stat, s_rcp);
+    }
 }
 
 template <bool HASH, int DK, int CK, bool OW1, int NZ = 8>
@@ -840,7 +868,7 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
     const Frame& fr = bt.f[tf];
     float* pyr = (float*)fr.pyr;
     const int t = threadIdx.x, r = t >> 4, c = t & 15;
-    if (count && t == 0 && tx == 0 && ty == 0 && tf == 0) coh_store(count, 0u);
+    if (count && t <= kMaxBatch && tx == 0 && ty == 0 && tf == 0) coh_store(count + t, 0u);  // class counters
     const int x0 = tx * 64 + c * 4, y0 = ty * 64 + r * 2;
     float ma = 0.0f, mb = 0.0f;  // level-1 texels (x0/2, y0/2) and (x0/2 + 1, y0/2)
     if (x0 < fr.W) {
@@ -903,7 +931,7 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
     float* pyr = (float*)fr.pyr;
     unsigned* rgbx = (unsigned*)fr.rgbx;
     const int t = threadIdx.x, r = t >> 5, c = t & 31;
-    if (count && t == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count, 0u);
+    if (count && t <= kMaxBatch && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count + t, 0u);
     const int x0 = blockIdx.x * 64 + c * 2, y0 = blockIdx.y * 64 + r * 2;
     float m1 = 0.0f;
 #pragma unroll

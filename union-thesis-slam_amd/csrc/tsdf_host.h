@@ -56,6 +56,7 @@ struct Profiler {
 // frames of batch j are staged in slot j % kSlots and stay there until the launch that
 // integrates them ends; the fourth slot lets the DMA of batch k+2 overlap launch k-1.
 constexpr int kSets = 3;
+constexpr int kCountWords = 16;  // per-set list counters (class c at word c)
 constexpr int kSlots = 4;
 
 // State common to the dense and hash handles.
@@ -69,7 +70,9 @@ struct Base {
     float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
     unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
     int pyr_H = 0, pyr_W = 0;
-    unsigned* list = nullptr;   // per-batch list of (brick | frame mask << 24) kept by the cull
+    // per-batch list of (brick | frame mask << 24) kept by the cull: kMaxBatch sub-lists of
+    // n_bricks entries, one per cost class (frames kept); count[c] = entries of class c (1..8)
+    unsigned* list = nullptr;
     unsigned int* count = nullptr;
     float* pyr_set[kSets] = {};
     unsigned* rgbx_set[kSets] = {};
