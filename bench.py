@@ -175,7 +175,8 @@ def main():
         ach = alg_bytes / kernel_s / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "tsdf::k_integrate<HASH=false, u16 depth, rgb8, ow==1>",
+                "kernel": "tsdf::k_fused<ow==1, NZ=4>: integrates batch k (and culls k+1, preps k+2 "
+                          "in the same launch); bytes = batch k's integrate bytes only",
                 "kernel_avg_us": round(1e6 * kernel_s / st["kernel_launches"], 2),
                 "bytes_per_launch": round(alg_bytes / st["kernel_launches"]),
                 "launches": st["kernel_launches"]}
@@ -203,9 +204,10 @@ def main():
         vol.integrate_batch(dh, ch, K, Tinv[:ni], sync=True)
         ti = max_over_ranks(time.perf_counter() - t0)
         ingest = {"frames_per_s": round(ni / ti, 1), "frames": ni,
-                  "source": "pageable numpy arrays, page-locked per call, DMA into two alternating "
-                            "device slots overlapped with integrate (tsdf_dense_integrate_batch "
-                            "without TSDF_DEVICE_PTRS)"}
+                  "source": "pageable numpy arrays copied by host threads into page-locked bounce "
+                            "slots, DMA on a copy stream into four device staging slots, overlapped "
+                            "with the pipelined launches (tsdf_dense_integrate_batch without "
+                            "TSDF_DEVICE_PTRS)"}
         log(f"[rank {rank}] ingest: {ni} host frames in {ti * 1e3:.1f} ms -> {ni / ti:.0f} frames/s")
     # ---- mesh extraction of the fused volume (not part of `value`) ----
     mesh = None

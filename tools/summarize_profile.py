@@ -47,7 +47,10 @@ def main(tag="r01"):
         summary["kernels"][k] = {"fetch_bytes_raw": fk, "fetch_bytes_corrected": 2 * fk,
                                  "write_bytes": wk, "hbm_bytes": 2 * fk + wk,
                                  "launches_sampled": len(fetch.get(k, []))}
-        if k.startswith("tsdf::k_integrate<false"):
+        # the dense integrate launch: k_fused (pipelined; also culls k+1 / preps k+2) or the
+        # in-line k_integrate<false, ...>
+        if k.startswith("tsdf::k_fused<true") or (k.startswith("tsdf::k_integrate<false")
+                                                  and "kernel" not in summary):
             summary["hbm_bytes_per_launch"] = round(2 * fk + wk)
             summary["kernel"] = k
     with open(os.path.join(dst, f"pmc_integrate_{tag}.json"), "w") as f:
