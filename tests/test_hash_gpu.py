@@ -226,3 +226,41 @@ def test_hash_batch_without_host_sync_matches_dense(hf):
         assert np.array_equal(a, b)
     sg, sh = g.stats(), h.stats()
     assert sg["voxel_updates"] == sh["voxel_updates"] and sh["lookups"] >= sh["blocks_allocated"] > 0
+
+
+@pytest.mark.parametrize("n_shards", [1, 2])
+def test_fused_and_inline_hash_with_growth_match_dense(hf, monkeypatch, n_shards):
+    """u16 + RGB8 hash calls run as three-stage launches (k_fused_hash: integrate batch k, cull
+    k+1, prep k+2; the last integrate workgroup commits the pool); TSDF_PIPELINE=0 forces the
+    in-line kernels.  20 frames in ONE synchronous call (3 batches) into a 37-slot table and a
+    16-block pool: both grow between batches, after the next batch's cull already ran.  Every
+    path and every shard pair must equal the dense grid (bucket-range ownership is fixed at
+    create, so a resize does not move blocks between shards)."""
+    from tsdf_amd import grid_fusion, scene
+    poses = scene.trajectory(20, seed=0, start=610)
+    d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=610)
+    d, c = np.ascontiguousarray(d.numpy()), np.ascontiguousarray(c.numpy())
+    K = scene.intrinsics()
+    bnds = np.array([[0.0, 10.24]] * 3)
+    Tinv = np.linalg.inv(poses)
+    g = grid_fusion.TSDFVolume(bnds.copy(), 0.08)
+    g.integrate_batch(d, c, K, Tinv)
+    G = g.get_state()
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("TSDF_PIPELINE", pipe)
+        hs = [hf.HashTable(bnds.copy(), 0.08, 37, max_blocks=16, shard=s, n_shards=n_shards)
+              for s in range(n_shards)]
+        for h in hs:
+            h.integrate_batch(d, c, K, Tinv)
+            # bricks_skipped counts first attempts that found no room; the synchronous call
+            # grew the table / pool and re-ran them before the next batch
+            assert h.stats()["bricks_skipped"] > 0 and h.info()["capacity"] > 37
+        S = [h.get_state() for h in hs]
+        if n_shards == 2:
+            assert not ((S[0][1] > 0) & (S[1][1] > 0)).any()
+        own = [s[1] > 0 for s in S]
+        for k in range(3):
+            merged = S[0][k].copy()
+            for s, o in zip(S[1:], own[1:]):
+                merged[o] = s[k][o]
+            assert np.array_equal(merged, G[k]), (pipe, k)

@@ -66,6 +66,9 @@ struct Frame {
 // updates are still applied frame by frame, in order, so results are those of one-by-one
 // integration; the brick state is read and written once per batch instead of once per frame).
 constexpr int kMaxBatch = 8;
+// Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
+// (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
+constexpr int kCountWords = 16, kDoneWord = 12;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 
 // w is an integer small enough that w + kMaxBatch indexes the reciprocal table
@@ -104,6 +107,7 @@ struct Table {
     int* overflow;              // list entries (brick | frame mask << 24) skipped this launch
     PoolState* st;
     long long capacity;
+    long long shard_cap;        // capacity at create: bucket-range ownership stays fixed across resizes
     long long max_blocks;
     int overflow_cap;
     int int_bits;               // 64: NumPy int64; 32: wrapping int32 (author's Windows run)
@@ -744,8 +748,8 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         if (cull_brick(v, fr, brick_box(v, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
             bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
             if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership
-                const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
-                test = (int)((home * v.n_shards) / tab.capacity) == v.shard;
+                const long long home = ref_hash(bx, by, bz, tab.shard_cap, tab.int_bits);
+                test = (int)((home * v.n_shards) / tab.shard_cap) == v.shard;
             }
             if (test && cull_brick(v, fr, brick_box(v, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
         }
@@ -874,7 +878,7 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
     const Frame& fr = bt.f[tf];
     float* pyr = (float*)fr.pyr;
     const int t = threadIdx.x, r = t >> 4, c = t & 15;
-    if (count && t <= kMaxBatch && tx == 0 && ty == 0 && tf == 0) coh_store(count + t, 0u);  // class counters
+    if (count && t < kCountWords && tx == 0 && ty == 0 && tf == 0) coh_store(count + t, 0u);  // list counters
     const int x0 = tx * 64 + c * 4, y0 = ty * 64 + r * 2;
     float ma = 0.0f, mb = 0.0f;  // level-1 texels (x0/2, y0/2) and (x0/2 + 1, y0/2)
     if (x0 < fr.W) {
@@ -937,7 +941,7 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
     float* pyr = (float*)fr.pyr;
     unsigned* rgbx = (unsigned*)fr.rgbx;
     const int t = threadIdx.x, r = t >> 5, c = t & 31;
-    if (count && t <= kMaxBatch && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count + t, 0u);
+    if (count && t < kCountWords && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) coh_store(count + t, 0u);
     const int x0 = blockIdx.x * 64 + c * 2, y0 = blockIdx.y * 64 + r * 2;
     float m1 = 0.0f;
 #pragma unroll
@@ -1027,6 +1031,57 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     } else if (b < sg.gi + sg.gc) {
         cull_superbrick<false>(v, bc, no_table, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
                                s_stat);
+    } else {
+        const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
+        const int f = t / per, r = t - f * per;
+        float(*sa)[33] = (float(*)[33])s_buf;
+        prep_vec_tile(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
+    }
+}
+
+// Fold one launch's allocations (PoolState::cursor) into the free list / bump pointer (the
+// hash's k_commit, also run by the last integrate workgroup of a fused hash launch).
+__device__ inline void commit_pool(PoolState* st, long long max_blocks) {
+    const long long used = coh_load(&st->cursor);
+    const long long nf = coh_load(&st->free_count);
+    const long long cons = used < nf ? used : nf;
+    const long long top = coh_load(&st->pool_top) + (used - cons);
+    coh_store(&st->free_count, nf - cons);
+    coh_store(&st->pool_top, top < max_blocks ? top : max_blocks);
+    coh_store(&st->cursor, 0ll);
+}
+
+// The voxel hash's three-stage launch (u16 + RGB8, obs_weight 1 as HashTable.integrate): as
+// k_fused, with the hash integrate (one wave per brick, in-kernel find-or-insert) and the pool
+// commit done by the integrate workgroup that finishes last (an arrival counter in the batch's
+// list counters; every workgroup's allocations are complete before it arrives).
+template <int = 0>
+__global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_fused_hash(
+        Vol v, Batch bi, Batch bc, Batch bp, Pool pool, Table tab, unsigned long long* stats, Stage sg) {
+    __shared__ double s_buf[kRcpTab];
+    __shared__ unsigned long long s_stat[kNStat];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, b = blockIdx.x;
+    if (b < sg.gi) {
+        if (tid < kNStat) s_stat[tid] = 0;
+        for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
+        __syncthreads();
+        constexpr int wpg = kFusedWG / 64;
+        integrate_list<true, 0, 0, true, 8>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
+                                            sg.gi * wpg, s_stat, s_buf);
+        __syncthreads();
+        flush_stats(s_stat, stats);
+        if (tid == 0) {
+            __threadfence();  // this workgroup's allocations and stores before its arrival
+            s_last = atomicAdd(sg.count_i + kDoneWord, 1u) == (unsigned)sg.gi - 1;
+        }
+        __syncthreads();
+        if (s_last && tid == 0) {
+            __threadfence();
+            commit_pool(tab.st, tab.max_blocks);
+        }
+    } else if (b < sg.gi + sg.gc) {
+        cull_superbrick<true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf, s_stat);
     } else {
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;

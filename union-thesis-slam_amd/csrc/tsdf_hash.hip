@@ -22,6 +22,7 @@ struct tsdf_hash {
     PoolState host_st{};
     unsigned* d_list = nullptr;  // re-run list
     int list_cap = 0;
+    bool fused = true;  // three-stage launches (k_fused_hash) when a call allows them
 };
 
 namespace {
@@ -37,15 +38,7 @@ __global__ void k_fill_keys(unsigned long long* k, long long n) {
 }
 
 // After each allocating launch: fold the launch's allocations into the pool state.
-__global__ void k_commit(PoolState* st, long long max_blocks) {
-    const long long used = coh_load(&st->cursor);
-    const long long nf = coh_load(&st->free_count);
-    const long long cons = used < nf ? used : nf;
-    const long long top = coh_load(&st->pool_top) + (used - cons);
-    coh_store(&st->free_count, nf - cons);
-    coh_store(&st->pool_top, top < max_blocks ? top : max_blocks);
-    coh_store(&st->cursor, 0ll);
-}
+__global__ void k_commit(PoolState* st, long long max_blocks) { commit_pool(st, max_blocks); }
 
 // Single-thread linear probe; returns the slot or -1.
 __device__ long long probe_find(const Table& t, unsigned long long key, long long home) {
@@ -376,6 +369,100 @@ void launch_integrate(tsdf_hash* h, const Batch& bt, int dk, int ck, const unsig
     }
 }
 
+// Synchronous calls: recover from a full table/pool exactly (the skipped bricks of batch `bt`
+// were not touched by any of its frames), then keep the reference's load-factor policy.
+int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
+    Base& B = h->b;
+    TSDF_TRY(read_state(h));
+    for (int round = 0; h->host_st.n_overflow > 0 && round < 40; ++round) {
+        const long long n_ov = h->host_st.n_overflow;
+        if (n_ov > h->t.overflow_cap)
+            return set_error(TSDF_E_CAPACITY, "overflow list exceeded (%lld bricks)", n_ov);
+        if (h->list_cap < n_ov) {
+            if (h->d_list) (void)hipFree(h->d_list);
+            TSDF_HIP(hipMalloc(&h->d_list, sizeof(unsigned) * n_ov));
+            h->list_cap = (int)n_ov;
+        }
+        TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(unsigned) * n_ov, hipMemcpyDeviceToDevice, B.stream));
+        TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
+        if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
+            TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
+        else
+            TSDF_TRY(resize_table(h, h->t.capacity * 2));
+        launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
+        TSDF_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+        TSDF_HIP(hipGetLastError());
+        TSDF_TRY(read_state(h));
+    }
+    if (h->host_st.n_overflow > 0) return set_error(TSDF_E_CAPACITY, "could not make room in the hash table");
+    return TSDF_OK;
+}
+
+// Three-stage launches (k_fused_hash; the dense path's scheme, tsdf_dense.hip): launch L
+// integrates batch L, culls L+1 and preps L+2.  Synchronous calls check batch L's overflow
+// before launch L+1 is issued; its re-run reads batch L's frames, which no launch has replaced.
+// The cull of batch L+1 already ran, which a resize cannot invalidate: it reads the table only
+// for shard ownership, fixed at create (Table::shard_cap).
+int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, const void* color, int H, int W,
+                   const double* K, const double* Tinv, int flags) {
+    Base& B = h->b;
+    const bool sync = !(flags & TSDF_ASYNC);
+    TSDF_TRY(B.use_sets(kSets));
+    const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
+    const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedWG);
+    const int gc_full = (int)B.cull_grid();
+    Batch bts[kSets];
+    for (int L = -2; L < nb; ++L) {
+        const int jp = L + 2;
+        if (jp < nb) {
+            const int f0 = jp * kMaxBatch;
+            const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+            B.use_set(jp % kSets);
+            // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
+            TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, TSDF_DEPTH_U16_MM, color, TSDF_COLOR_RGB8, H, W,
+                                     K, Tinv, nullptr, 1.0, flags, f0, n, jp % kSlots));
+        }
+        const bool has_i = L >= 0, has_c = L + 1 >= 0 && L + 1 < nb, has_p = jp < nb;
+        static const Batch kNone{};
+        const Batch& bi = has_i ? bts[L % kSets] : kNone;
+        const Batch& bc = has_c ? bts[(L + 1) % kSets] : kNone;
+        const Batch& bp = has_p ? bts[jp % kSets] : kNone;
+        Stage sg{};
+        sg.gi = has_i ? gi_full : 0;
+        sg.gc = has_c ? gc_full : 0;
+        sg.ptx = (W + 63) / 64;
+        sg.pty = (H + 63) / 64;
+        if (has_i) {
+            sg.list_i = B.list_set[L % kSets];
+            sg.count_i = B.count_set[L % kSets];
+        }
+        if (has_c) {
+            sg.list_c = B.list_set[(L + 1) % kSets];
+            sg.count_c = B.count_set[(L + 1) % kSets];
+        }
+        if (has_p) sg.count_p = B.count_set[jp % kSets];
+        const long long grid = (long long)sg.gi + sg.gc + (has_p ? (long long)sg.ptx * sg.pty * bp.n : 0);
+        if (grid >= (1ll << 31)) return set_error(TSDF_E_ARG, "fused grid too large");
+        hipEvent_t e0 = nullptr;
+        if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
+        hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, bc, bp,
+                           B.pool, h->t, B.stats, sg);
+        TSDF_HIP(hipGetLastError());
+        if (!has_i) continue;
+        TSDF_TRY(B.prof.end(B.stream, e0));
+        B.frames += bi.n;
+        if (sync) {
+            TSDF_TRY(hash_after_batch(h, bi, TSDF_DEPTH_U16_MM, TSDF_COLOR_RGB8));
+            TSDF_TRY(B.end_batch(flags, L % kSlots));
+            TSDF_TRY(ensure_room(h));
+        } else {
+            TSDF_TRY(B.end_batch(flags, L % kSlots));
+        }
+    }
+    return TSDF_OK;
+}
+
 int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int ck,
              int H, int W, const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
@@ -385,6 +472,16 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
+    bool fused = h->fused && dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
+    if (fused && (flags & TSDF_DEVICE_PTRS))
+        fused = (uintptr_t)depth % 8 == 0 && (uintptr_t)color % 4 == 0 && ((size_t)H * W) % 4 == 0;
+    if (fused) {
+        TSDF_TRY(hash_run_fused(h, n_frames, depth, color, H, W, K, Tinv, flags));
+        TSDF_TRY(guard.finish());
+        if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
+        return TSDF_OK;
+    }
+    B.use_set(0);
     for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
         Batch bt;
         const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
@@ -407,31 +504,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
             TSDF_TRY(B.end_batch(flags, slot));
             continue;
         }
-        // Synchronous: recover from a full table/pool exactly (the skipped bricks were not
-        // touched by any frame of the batch), then keep the reference's load-factor policy.
-        TSDF_TRY(read_state(h));
-        for (int round = 0; h->host_st.n_overflow > 0 && round < 40; ++round) {
-            const long long n_ov = h->host_st.n_overflow;
-            if (n_ov > h->t.overflow_cap)
-                return set_error(TSDF_E_CAPACITY, "overflow list exceeded (%lld bricks)", n_ov);
-            if (h->list_cap < n_ov) {
-                if (h->d_list) (void)hipFree(h->d_list);
-                TSDF_HIP(hipMalloc(&h->d_list, sizeof(unsigned) * n_ov));
-                h->list_cap = (int)n_ov;
-            }
-            TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(unsigned) * n_ov, hipMemcpyDeviceToDevice, B.stream));
-            TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
-            if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
-                TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
-            else
-                TSDF_TRY(resize_table(h, h->t.capacity * 2));
-            launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
-            TSDF_HIP(hipGetLastError());
-            hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
-            TSDF_HIP(hipGetLastError());
-            TSDF_TRY(read_state(h));
-        }
-        if (h->host_st.n_overflow > 0) return set_error(TSDF_E_CAPACITY, "could not make room in the hash table");
+        TSDF_TRY(hash_after_batch(h, bt, dk, ck));
         TSDF_TRY(B.end_batch(flags, slot));  // the overflow re-runs above read this batch's frames
         TSDF_TRY(ensure_room(h));
     }
@@ -495,6 +568,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         if (max_blocks <= 0) max_blocks = std::min<long long>(h->b.n_bricks, 1 << 16);
         max_blocks = std::max<long long>(max_blocks, 64);
         t.capacity = capacity;
+        t.shard_cap = capacity;
         t.max_blocks = max_blocks;
         t.int_bits = int_bits;
         t.overflow_cap = (int)std::min<long long>(h->b.n_bricks, 1ll << 30);
@@ -511,6 +585,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
             r = set_error(e == hipErrorOutOfMemory ? TSDF_E_OOM : TSDF_E_HIP, "hash allocation: %s",
                           hipGetErrorString(e));
     }
+    if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;  // 0: in-line kernels
     if (r == TSDF_OK) r = tsdf_hash_reset(h);
     if (r != TSDF_OK) {
         std::string keep = tsdf_last_error();

@@ -56,7 +56,6 @@ struct Profiler {
 // frames of batch j are staged in slot j % kSlots and stay there until the launch that
 // integrates them ends; the fourth slot lets the DMA of batch k+2 overlap launch k-1.
 constexpr int kSets = 3;
-constexpr int kCountWords = 16;  // per-set list counters (class c at word c)
 constexpr int kSlots = 4;
 
 // State common to the dense and hash handles.

@@ -61,7 +61,9 @@ def ref_hash(x, y, z, n: int, int_bits: int = 64):
 
 def hash_owner(bx, by, bz, capacity: int, n_shards: int, int_bits: int = 64):
     """Shard owning block (bx,by,bz): the bucket range its home slot falls in (the same
-    arithmetic as k_cull<true>)."""
+    arithmetic as k_cull<true>).  `capacity` is the table's capacity at create: ownership is
+    fixed then (Table::shard_cap) and does not follow later resizes, so no block ever moves
+    between shards."""
     home = ref_hash(bx, by, bz, capacity, int_bits)
     return (home * n_shards) // capacity
 
