@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=1000, help="synthetic frames resident in HBM")
     ap.add_argument("--no-hash", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=5, help="CPU-baseline sample (~2 s per frame)")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host-frame (PCIe) measurement")
     ap.add_argument("--ingest-frames", type=int, default=256)
@@ -109,10 +109,21 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if n > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
+        # the backends' connection messages go to fd 1 (gloo prints "Rank r is connected to ...");
+        # send them to stderr so that stdout carries only the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(args.dist_backend)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     def barrier():

@@ -824,9 +824,9 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
     }
 }
 
-// Occupancy targets (waves per SIMD) of the integrate kernels.  Dense: 6 (<= 80 VGPRs; with
-// 512-thread k_fused workgroups that is 3 per CU, 99 KB of LDS) -- measured 8 % faster than 4
-// at 512^3; 8 would spill to scratch.  Hash (NZ = 8, the probe state): 4.
+// Occupancy targets (waves per SIMD) of the integrate kernels.  Dense k_fused: 6 (<= 80 VGPRs;
+// 512-thread workgroups, 3 per CU, 99 KB of LDS) -- measured 8 % faster than 4 at 512^3
+// (DESIGN.md §4); 8 would spill to scratch.  Hash (NZ = 8, the probe state) and in-line: 4.
 #ifndef TSDF_DENSE_WAVES
 #define TSDF_DENSE_WAVES 6
 #endif
@@ -834,7 +834,9 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
 #define TSDF_HASH_WAVES 4
 #endif
 template <bool HASH, int DK, int CK, bool OW1, int NZ = 8>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(HASH ? TSDF_HASH_WAVES : TSDF_DENSE_WAVES))) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
+// (the in-line k_integrate: 256-thread workgroups with a 32 KB LDS table fit 4 per CU, so 4 waves
+// per SIMD whatever the registers allow)
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
                                                   unsigned long long* stats, const unsigned* list,
                                                   unsigned int* count, int n_list) {
     __shared__ unsigned long long s_stat[kNStat];
