@@ -1,5 +1,5 @@
-# Prep/cull pipeline A/B: GPU tests with the pipeline forced on, then the shard ranks of 2/4/8-way
-# cyclic sharding and the full volume with TSDF_PIPELINE=0 and =1.
+# Fused three-stage launch (TSDF_PIPELINE=1, default) vs the in-line kernels (=0): GPU tests with
+# the in-line path forced, then rank 0 of the 2/4/8-way cyclic shards and the full volume under both.
 set -o pipefail
 mkdir -p gpurun_out/pipe
 TSDF_PIPELINE=1 timeout -k 10 300 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pipe/tests_pipe1.log 2>&1 || exit $?
