@@ -484,7 +484,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
             const double rz = refined_rcp(z);
-            const double sx = (x * fr.fx) * rz + fr.cx, sy = (y * fr.fy) * rz + fr.cy;
+            // one FMA for (x*fx)*rz + cx: within ~1e-11 px of the reference's (x*fx)/z + cx
+            // either way, far inside the 1e-9 px boundary margin below
+            const double sx = fma(x * fr.fx, rz, fr.cx), sy = fma(y * fr.fy, rz, fr.cy);
             const double ux = rint(sx), uy = rint(sy);
             // (a NaN fails both tests; far-out |s| may round differently but is invalid either way)
             const bool ok = fabs(sx - ux) < 0.5 - 1e-9 && fabs(sy - uy) < 0.5 - 1e-9;
