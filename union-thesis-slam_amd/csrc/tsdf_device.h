@@ -441,7 +441,13 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     // vox2world (grid_fusion.py:170-181); lanes 0..7 compute the brick's 8 z coordinates
     const double px = vox_world(v.origin[0], v.vs, v.off[0] + bx * v.xstride + (lane >> 3));
     const double py = vox_world(v.origin[1], v.vs, v.off[1] + ly);
-    const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));  // lane k: z = k (zoff added at use)
+    const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));  // lane k: z = k
+    // z-part waves (NZ = 4, dense): this part's z coordinates read out of the lanes once per item
+    // (+1.5 %); with NZ = 8 the hash kernel has no registers to spare and reads them per frame
+    constexpr int kPz = NZ < 8 ? NZ : 1;
+    double pzs[kPz];
+#pragma unroll
+    for (int k = 0; k < kPz; ++k) pzs[k] = readlane_f64(pz_l, k + zoff);
 
     float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
@@ -479,7 +485,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         unsigned inb = 0, slow = 0;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            const double pz = readlane_f64(pz_l, k + zoff);
+            const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
             const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
@@ -501,7 +507,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #pragma unroll
             for (int k = 0; k < NZ; ++k) {
                 if (!((slow >> k) & 1u)) continue;
-                const double pz = readlane_f64(pz_l, k + zoff);
+                const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
                 const double x = fr.T[3] + fma(fr.T[2], pz, a0);
                 const double y = fr.T[7] + fma(fr.T[6], pz, a1);
                 uu[k] = rint((x * fr.fx) / zc[k] + fr.cx);  // the reference's own operation order
