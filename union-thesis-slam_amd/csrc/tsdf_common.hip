@@ -145,7 +145,7 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
         TSDF_HIP(hipEventRecord(ev_copied[k], cstream));
     }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    TSDF_HIP(hipMalloc(&list_set[0], sizeof(unsigned) * (size_t)n_bricks * kMaxBatch));
+    TSDF_HIP(hipMalloc(&list_set[0], sizeof(ListEntry) * (size_t)n_bricks * kMaxBatch));
     TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
     TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * kCountWords, stream));
     use_set(0);
@@ -163,7 +163,7 @@ int Base::use_sets(int n) {
     if (n <= n_sets) return TSDF_OK;
     TSDF_TRY(sync_all());
     for (int k = n_sets; k < n; ++k) {
-        TSDF_HIP(hipMalloc(&list_set[k], sizeof(unsigned) * (size_t)n_bricks * kMaxBatch));
+        TSDF_HIP(hipMalloc(&list_set[k], sizeof(ListEntry) * (size_t)n_bricks * kMaxBatch));
         TSDF_HIP(hipMalloc(&count_set[k], sizeof(unsigned int) * kCountWords));
         TSDF_HIP(hipMemsetAsync(count_set[k], 0, sizeof(unsigned int) * kCountWords, stream));
     }
@@ -323,11 +323,11 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->pyr = pyr + (size_t)lay.total * i;
 
         frustum_planes(fr, T, W, H);
-        for (int L = 0; L <= kPyrLevels; ++L) {
-            fr->pyr_off[L] = lay.off[L];
-            fr->pyr_w[L] = lay.w[L];
-            fr->pyr_h[L] = lay.h[L];
-        }
+    }
+    for (int L = 0; L <= kPyrLevels; ++L) {
+        bt->pg.off[L] = lay.off[L];
+        bt->pg.w[L] = lay.w[L];
+        bt->pg.h[L] = lay.h[L];
     }
     return TSDF_OK;
 }

@@ -66,7 +66,7 @@ int dense_run_inline(tsdf_dense* h, int n_frames, const void* depth, int dk, con
         TSDF_TRY(B.prof.begin(B.stream, &e0));
         bool ow1 = true;
         for (int i = 0; i < n; ++i) ow1 = ow1 && bt.f[i].ow == 1.0;
-        const unsigned* L = (const unsigned*)B.list;
+        const ListEntry* L = B.list;
         const int sel = (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (ck == TSDF_COLOR_RGB8 ? 0 : 2) | (ow1 ? 1 : 0) |
                         (h->nz == 4 ? 8 : 0);
         switch (sel) {

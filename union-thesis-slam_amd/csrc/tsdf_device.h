@@ -57,18 +57,27 @@ struct Frame {
     const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
     float planes[5][4];       // world-space half-spaces containing every valid voxel (cull)
-    int pyr_off[kPyrLevels + 1];
-    int pyr_w[kPyrLevels + 1];
-    int pyr_h[kPyrLevels + 1];
+};
+
+// Layout of a frame's max-depth pyramid (levels 1..kPyrLevels concatenated), the same for every
+// frame of a batch.
+struct PyrGeo {
+    int off[kPyrLevels + 1];
+    int w[kPyrLevels + 1];
+    int h[kPyrLevels + 1];
 };
 
 // Up to kMaxBatch consecutive frames integrated by one launch (temporal batching: each voxel's
 // updates are still applied frame by frame, in order, so results are those of one-by-one
 // integration; the brick state is read and written once per batch instead of once per frame).
-constexpr int kMaxBatch = 8;
+#ifndef TSDF_MAX_BATCH
+#define TSDF_MAX_BATCH 8
+#endif
+constexpr int kMaxBatch = TSDF_MAX_BATCH;
+static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
-constexpr int kCountWords = 16, kDoneWord = 12;
+constexpr int kCountWords = 32, kDoneWord = 24;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 
 // w is an integer small enough that w + kMaxBatch indexes the reciprocal table
@@ -81,8 +90,12 @@ __device__ inline bool canon_color(float c) {
 }
 struct Batch {
     Frame f[kMaxBatch];
+    PyrGeo pg;
     int n;
 };
+
+// A culled brick for the integrate: brick index (low 32 bits) | frames that kept it << 32.
+typedef unsigned long long ListEntry;
 
 // Brick storage: SoA pool of 512-voxel bricks.
 struct Pool {
@@ -104,7 +117,7 @@ struct Table {
     int* vals;                  // pool block of each slot
     unsigned long long* occ;    // [max_blocks][8] voxel-entry bits (word = z, bit = x*8+y)
     int* free_list;
-    int* overflow;              // list entries (brick | frame mask << 24) skipped this launch
+    ListEntry* overflow;        // list entries skipped this launch
     PoolState* st;
     long long capacity;
     long long shard_cap;        // capacity at create: bucket-range ownership stays fixed across resizes
@@ -190,7 +203,7 @@ __device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz, int n
     return r;
 }
 
-__device__ inline bool cull_brick(const Vol& v, const Frame& fr, const BrickBox& bb) {
+__device__ inline bool cull_brick(const Vol& v, const Frame& fr, const PyrGeo& pg, const BrickBox& bb) {
     // early out: the brick's bounding sphere entirely outside one of the frustum half-spaces
     // (z > 0 and -0.5 <= u < W - 0.5, -0.5 <= v < H - 0.5, each widened by 1 px)
 #pragma unroll
@@ -238,8 +251,8 @@ __device__ inline bool cull_brick(const Vol& v, const Frame& fr, const BrickBox&
     const float need = zmin - (float)v.trunc - 1e-3f;
     const int tx0 = u0 >> L, tx1 = u1 >> L, ty0 = v0 >> L, ty1 = v1 >> L;
     if (tx1 - tx0 > 3 || ty1 - ty0 > 3) return true;
-    const float* lvl = fr.pyr + fr.pyr_off[L];
-    const int wl = fr.pyr_w[L];
+    const float* lvl = fr.pyr + pg.off[L];
+    const int wl = pg.w[L];
     float dmax = 0.0f;
 #pragma unroll
     for (int dy = 0; dy < 4; ++dy)
@@ -418,13 +431,13 @@ __device__ inline unsigned halves_of(unsigned m) {
 
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
-                                       const Table& tab, unsigned entry, int zoff,
+                                       const Table& tab, ListEntry entry, int zoff,
                                        unsigned long long* s_stat, const double* s_rcp) {
     static_assert(NZ == 8 || (NZ == 4 && !HASH), "z-split parts are dense-only");
     constexpr unsigned kHalves = NZ == 8 ? 3u : 1u;
     const int lane = lane_id();
-    const int b = (int)(entry & 0xFFFFFFu);
-    const unsigned fmask = entry >> 24;
+    const int b = (int)(entry & 0xFFFFFFFFull);
+    const unsigned fmask = (unsigned)(entry >> 32);
     const int nb12 = v.nb[1] * v.nb[2];
     if (b >= v.nb[0] * nb12) {  // never for a list k_cull wrote; guards the pool against bad input
         if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
@@ -564,7 +577,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 if (r < 0) {  // no space: skip the brick for the whole batch (nothing written yet);
                     if (lane == 0) {  // the host grows the table and re-runs it
                         const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
-                        if ((long long)o < tab.overflow_cap) tab.overflow[o] = (int)entry;
+                        if ((long long)o < tab.overflow_cap) tab.overflow[o] = entry;
                         atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
                     }
                     return;
@@ -728,7 +741,7 @@ __device__ inline void flush_stats(unsigned long long* s_stat, unsigned long lon
 // Conservative cull of every brick (one lane each) against every frame of the batch, and
 // compaction of the bricks seen by at least one frame into a list of (brick | frame mask << 24):
 // wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
-constexpr int kCullWG = 64 * kMaxBatch;  // k_cull: one wave per frame of the batch
+constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 8
 
 // Brick culling for one batch, hierarchical: one workgroup per superbrick (64 bricks, Vol::sb),
 // one wave per frame.  Wave f tests the superbrick against frame f (wave-uniform) and, if it
@@ -736,11 +749,11 @@ constexpr int kCullWG = 64 * kMaxBatch;  // k_cull: one wave per frame of the ba
 // wave 0 appends the kept bricks to the list (one atomicAdd per superbrick with survivors).
 // Every test is at most two cull_brick latencies deep, whatever the batch size.
 template <bool HASH>
-__device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Table& tab, unsigned* list,
+__device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Table& tab, ListEntry* list,
                                        unsigned int* count, unsigned long long* stats, int si,
                                        unsigned* s_mask, unsigned long long* s_stat) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int f = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int f0 = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid < 64) s_mask[tid] = 0u;
     if (tid < kNStat) s_stat[tid] = 0;
     __syncthreads();
@@ -751,15 +764,15 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
     const int lz = lane & (ez - 1), ly = (lane >> v.sb[2]) & (ey - 1), lx = lane >> (v.sb[1] + v.sb[2]);
     const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
     const unsigned e = (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz);
-    if (f < bt.n) {
+    for (int f = f0; f < bt.n; f += kCullWG / 64) {  // wave w: frames w, w + 8
         const Frame& fr = bt.f[f];
-        if (cull_brick(v, fr, brick_box(v, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
+        if (cull_brick(v, fr, bt.pg, brick_box(v, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
             bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
             if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership
                 const long long home = ref_hash(bx, by, bz, tab.shard_cap, tab.int_bits);
                 test = (int)((home * v.n_shards) / tab.shard_cap) == v.shard;
             }
-            if (test && cull_brick(v, fr, brick_box(v, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
+            if (test && cull_brick(v, fr, bt.pg, brick_box(v, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
         }
     }
     __syncthreads();
@@ -780,7 +793,8 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
             if (lane == 0) s_stat[ST_VISITED] = (unsigned long long)__popcll(any);
             base = __shfl(base, cls);
             const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
-            if (cls && base + rank < nbk) list[(size_t)(cls - 1) * nbk + base + rank] = e | (fmask << 24);
+            if (cls && base + rank < nbk)
+                list[(size_t)(cls - 1) * nbk + base + rank] = (ListEntry)e | ((ListEntry)fmask << 32);
         }
     }
     __syncthreads();
@@ -788,7 +802,7 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
 }
 
 template <bool HASH>
-__global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, unsigned* list,
+__global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, ListEntry* list,
                                                   unsigned int* count, unsigned long long* stats) {
     __shared__ unsigned s_mask[64];
     __shared__ unsigned long long s_stat[kNStat];
@@ -801,7 +815,7 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, un
 // used (hash overflow re-run).
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
-                                      const unsigned* list, unsigned int* count, int n_list, int wave,
+                                      const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
@@ -845,7 +859,7 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ = 8>
 // (the in-line k_integrate: 256-thread workgroups with a 32 KB LDS table fit 4 per CU, so 4 waves
 // per SIMD whatever the registers allow)
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
-                                                  unsigned long long* stats, const unsigned* list,
+                                                  unsigned long long* stats, const ListEntry* list,
                                                   unsigned int* count, int n_list) {
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ double s_rcp[OW1 ? kRcpTab : 1];  // RN(1/n): weights are small integers when ow == 1
@@ -866,7 +880,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_W
 // (texel = max over a 2^L x 2^L block, metres, 0 for invalid/outside) and the reset of the
 // brick-list counter.  One 1024-thread workgroup per 64x64 tile, 2x2 pixels per thread.
 template <int REDUCE>
-__device__ inline void pyr_level(const Frame& fr, float* pyr, int L, const float (*src)[33],
+__device__ inline void pyr_level(const PyrGeo& pg, float* pyr, int L, const float (*src)[33],
                                  float (*dst)[33], int n, int tx = blockIdx.x, int ty = blockIdx.y) {
     const int t = threadIdx.x;
     if (t < n * n) {
@@ -875,7 +889,7 @@ __device__ inline void pyr_level(const Frame& fr, float* pyr, int L, const float
                               fmaxf(src[2 * rr + 1][2 * cc], src[2 * rr + 1][2 * cc + 1]));
         dst[rr][cc] = m;
         const int X = tx * n + cc, Y = ty * n + rr;
-        if (X < fr.pyr_w[L] && Y < fr.pyr_h[L]) pyr[fr.pyr_off[L] + Y * fr.pyr_w[L] + X] = m;
+        if (X < pg.w[L] && Y < pg.h[L]) pyr[pg.off[L] + Y * pg.w[L] + X] = m;
     }
 }
 
@@ -917,23 +931,24 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
     }
     {
         const int X = x0 >> 1, Y = y0 >> 1;
-        if (Y < fr.pyr_h[1]) {
-            if (X < fr.pyr_w[1]) pyr[fr.pyr_off[1] + Y * fr.pyr_w[1] + X] = ma;
-            if (X + 1 < fr.pyr_w[1]) pyr[fr.pyr_off[1] + Y * fr.pyr_w[1] + X + 1] = mb;
+        const PyrGeo& pg = bt.pg;
+        if (Y < pg.h[1]) {
+            if (X < pg.w[1]) pyr[pg.off[1] + Y * pg.w[1] + X] = ma;
+            if (X + 1 < pg.w[1]) pyr[pg.off[1] + Y * pg.w[1] + X + 1] = mb;
         }
     }
     sa[r][2 * c] = ma;
     sa[r][2 * c + 1] = mb;
     __syncthreads();
-    pyr_level<0>(fr, pyr, 2, sa, sb, 16, tx, ty);
+    pyr_level<0>(bt.pg, pyr, 2, sa, sb, 16, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 3, sb, sa, 8, tx, ty);
+    pyr_level<0>(bt.pg, pyr, 3, sb, sa, 8, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 4, sa, sb, 4, tx, ty);
+    pyr_level<0>(bt.pg, pyr, 4, sa, sb, 4, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 5, sb, sa, 2, tx, ty);
+    pyr_level<0>(bt.pg, pyr, 5, sb, sa, 2, tx, ty);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 6, sa, sb, 1, tx, ty);
+    pyr_level<0>(bt.pg, pyr, 6, sa, sb, 1, tx, ty);
 }
 
 template <int = 0>
@@ -981,19 +996,19 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
         }
     {
         const int X = (x0 >> 1), Y = (y0 >> 1);
-        if (X < fr.pyr_w[1] && Y < fr.pyr_h[1]) pyr[fr.pyr_off[1] + Y * fr.pyr_w[1] + X] = m1;
+        if (X < bt.pg.w[1] && Y < bt.pg.h[1]) pyr[bt.pg.off[1] + Y * bt.pg.w[1] + X] = m1;
     }
     sa[r][c] = m1;
     __syncthreads();
-    pyr_level<0>(fr, pyr, 2, sa, sb, 16);
+    pyr_level<0>(bt.pg, pyr, 2, sa, sb, 16);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 3, sb, sa, 8);
+    pyr_level<0>(bt.pg, pyr, 3, sb, sa, 8);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 4, sa, sb, 4);
+    pyr_level<0>(bt.pg, pyr, 4, sa, sb, 4);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 5, sb, sa, 2);
+    pyr_level<0>(bt.pg, pyr, 5, sb, sa, 2);
     __syncthreads();
-    pyr_level<0>(fr, pyr, 6, sa, sb, 1);
+    pyr_level<0>(bt.pg, pyr, 6, sa, sb, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1009,9 +1024,9 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
 constexpr int kFusedWG = 512;
 static_assert(kFusedWG == kCullWG, "a cull workgroup is one wave per frame of the batch");
 struct Stage {
-    const unsigned* list_i;  // integrate: list and count of batch k
+    const ListEntry* list_i;  // integrate: list and count of batch k
     unsigned int* count_i;
-    unsigned* list_c;        // cull: list and count of batch k+1
+    ListEntry* list_c;        // cull: list and count of batch k+1
     unsigned int* count_c;
     unsigned int* count_p;   // prep: count of batch k+2 (reset for its cull)
     int gi, gc;              // integrate / cull workgroups

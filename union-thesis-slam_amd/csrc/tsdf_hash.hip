@@ -20,7 +20,7 @@ struct tsdf_hash {
     Base b;
     Table t{};          // device view (pointers + capacity)
     PoolState host_st{};
-    unsigned* d_list = nullptr;  // re-run list
+    ListEntry* d_list = nullptr;  // re-run list
     int list_cap = 0;
     bool fused = true;  // three-stage launches (k_fused_hash) when a call allows them
 };
@@ -350,7 +350,7 @@ int ensure_room(tsdf_hash* h) {
 
 // One hash integrate pass over a batch: the listed bricks (list/count from k_cull, or an
 // explicit list of skipped entries).
-void launch_integrate(tsdf_hash* h, const Batch& bt, int dk, int ck, const unsigned* list,
+void launch_integrate(tsdf_hash* h, const Batch& bt, int dk, int ck, const ListEntry* list,
                       unsigned int* count, int n_list) {
     Base& B = h->b;
     const unsigned grid = B.grid_for((const void*)k_integrate<true, 0, 0, true>);
@@ -380,10 +380,10 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
             return set_error(TSDF_E_CAPACITY, "overflow list exceeded (%lld bricks)", n_ov);
         if (h->list_cap < n_ov) {
             if (h->d_list) (void)hipFree(h->d_list);
-            TSDF_HIP(hipMalloc(&h->d_list, sizeof(unsigned) * n_ov));
+            TSDF_HIP(hipMalloc(&h->d_list, sizeof(ListEntry) * n_ov));
             h->list_cap = (int)n_ov;
         }
-        TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(unsigned) * n_ov, hipMemcpyDeviceToDevice, B.stream));
+        TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(ListEntry) * n_ov, hipMemcpyDeviceToDevice, B.stream));
         TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
         if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
             TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
@@ -494,7 +494,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         TSDF_HIP(hipGetLastError());
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
-        launch_integrate(h, bt, dk, ck, (const unsigned*)B.list, B.count, 0);
+        launch_integrate(h, bt, dk, ck, B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
@@ -576,7 +576,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         if (e == hipSuccess) e = hipMalloc(&t.vals, sizeof(int) * capacity);
         if (e == hipSuccess) e = hipMalloc(&t.occ, sizeof(unsigned long long) * 8 * max_blocks);
         if (e == hipSuccess) e = hipMalloc(&t.free_list, sizeof(int) * max_blocks);
-        if (e == hipSuccess) e = hipMalloc(&t.overflow, sizeof(int) * (size_t)t.overflow_cap);
+        if (e == hipSuccess) e = hipMalloc(&t.overflow, sizeof(ListEntry) * (size_t)t.overflow_cap);
         if (e == hipSuccess) e = hipMalloc(&t.st, sizeof(PoolState));
         if (e == hipSuccess) e = hipMalloc(&h->b.pool.tsdf, sizeof(float) * kBrickVox * max_blocks);
         if (e == hipSuccess) e = hipMalloc(&h->b.pool.weight, sizeof(float) * kBrickVox * max_blocks);

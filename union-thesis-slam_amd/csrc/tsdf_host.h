@@ -71,11 +71,11 @@ struct Base {
     int pyr_H = 0, pyr_W = 0;
     // per-batch list of (brick | frame mask << 24) kept by the cull: kMaxBatch sub-lists of
     // n_bricks entries, one per cost class (frames kept); count[c] = entries of class c (1..8)
-    unsigned* list = nullptr;
+    ListEntry* list = nullptr;
     unsigned int* count = nullptr;
     float* pyr_set[kSets] = {};
     unsigned* rgbx_set[kSets] = {};
-    unsigned* list_set[kSets] = {};
+    ListEntry* list_set[kSets] = {};
     unsigned int* count_set[kSets] = {};
     unsigned short* dmask_set[kSets] = {};
     int n_sets = 1;             // buffer sets allocated (kSets once the fused pipeline is used)
