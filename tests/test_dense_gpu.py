@@ -259,12 +259,12 @@ def test_long_batch_without_host_sync_matches_oracle(gf):
     assert vol.stats()["list_errors"] == 0
 
 
-def test_host_ingest_double_buffered_equals_device_path(gf):
-    """Frame ingest: 21 host frames (3 batches, both staging slots, one
-    reused) from pageable numpy arrays and from a pinned torch tensor equal the device-resident
-    run bit for bit; the call returns with the host arrays no longer needed."""
+def test_host_ingest_staging_slots_equal_device_path(gf):
+    """Frame ingest: 45 host frames (6 batches over the four staging
+    slots, two of them reused) from pageable numpy arrays and from a pinned torch tensor equal
+    the device-resident run bit for bit; the call returns with the host arrays no longer needed."""
     import torch
-    d, c, poses = _synth(21, start=5)
+    d, c, poses = _synth(45, start=5)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     bnds = np.array([[0.0, 10.24]] * 3)
     Tinv = np.linalg.inv(poses)
@@ -348,3 +348,41 @@ def test_prep_cull_pipeline_on_and_off_bit_identical(gf, monkeypatch, ingest):
         states.append(vol.get_state())
     for a, b, e in zip(states[0], states[1], (orc._tsdf_vol_cpu, orc._weight_vol_cpu, orc._color_vol_cpu)):
         assert _same(a, e) and _same(b, e)
+
+
+def test_bench_workload_at_full_size_matches_oracle_rows(gf):
+    """The bench's own path at BASELINE size: 512^3 @ 2 cm, 40 synthetic frames resident in HBM,
+    one async call (five batches through the three-stage k_fused launches).  22 x-rows spread
+    over the volume (every residue mod 8, so every lane column of a brick) are checked bit-exact
+    against the oracle restricted to those rows; the hash path over the same frames must hold
+    the same state on those rows."""
+    torch = pytest.importorskip("torch")
+    from tsdf_amd import hash_fusion, scene
+    n = 40
+    d, c, poses = _synth(n, start=120)
+    K = scene.intrinsics()
+    bnds = np.array([[0.0, 10.24]] * 3)
+    Tinv = np.linalg.inv(poses)
+    dd = torch.from_numpy(np.ascontiguousarray(d).view(np.int16)).cuda()
+    cc = torch.from_numpy(np.ascontiguousarray(c)).cuda()
+    torch.cuda.synchronize()
+    vol = gf.TSDFVolume(bnds.copy(), 0.02)
+    assert tuple(int(x) for x in vol._vol_dim) == (512, 512, 512)
+    vol.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True, sync=False)
+    ht = hash_fusion.HashTable(bnds.copy(), 0.02, 1 << 22)
+    ht.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True, sync=False)
+    vol.sync()
+    ht.sync()
+    rows = np.arange(5, 512, 23)
+    assert len(np.unique(rows % 8)) == 8
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.02, x_index=rows)
+    n_upd = sum(orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f]) for f in range(n))
+    assert n_upd > 1_000_000
+    G = [a[rows] for a in vol.get_state()]
+    for a, o in zip(G, (orc._tsdf_vol_cpu, orc._weight_vol_cpu, orc._color_vol_cpu)):
+        assert _same(a, o)
+    Hs = [a[rows] for a in ht.get_state()]
+    for a, b in zip(G, Hs):
+        assert np.array_equal(a, b)
+    sg, sh = vol.stats(), ht.stats()
+    assert sg["list_errors"] == 0 and sg["voxel_updates"] == sh["voxel_updates"] > 0

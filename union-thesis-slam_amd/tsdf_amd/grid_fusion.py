@@ -175,8 +175,8 @@ class TSDFVolume:
         world_to_cam: (F,4,4) = inv(cam_pose) per frame, computed by the caller.
         depth_kind/color_kind default to u16 mm / RGB8 for device pointers and are taken from
         the dtype of host arrays (u16|i16 mm or f64 m; (F,H,W,3) u8 or folded (F,H,W) f32).
-        Host arrays are page-locked for the call and copied by DMA into two alternating device
-        slots while the previous batch integrates.  invalid_65535: u16 65535 mm is invalid (0),
+        Host arrays are copied by host threads into page-locked bounce slots and DMAed into
+        one of four device staging slots while earlier batches integrate.  invalid_65535: u16 65535 mm is invalid (0),
         the demos' `depth_im[depth_im == 65.535] = 0` (grid_demo1.py:82) done on the device."""
         depth, depth_kind, color, color_kind = frame_stack(depth, depth_kind, color, color_kind, device_ptrs)
         T = np.ascontiguousarray(np.asarray(world_to_cam, dtype=np.float64).reshape(-1, 16))
