@@ -370,11 +370,12 @@ __device__ inline double depth_m(const Frame& fr, int p, unsigned raw) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Reciprocal of z for the fast pixel path.  v_rcp_f64 is accurate to 2^-24.4 and one Newton step
-// brings it to 2^-48.7 (measured over z in [1e-3, 1e3]: tools/gpu/rcp_probe.hip),
-// so u = (x*fx)*rz + cx lies within ~1e-11 px of the reference's (x*fx)/z + cx wherever a pixel
-// can be valid (|u| < 1e3).  Steps whose u is within 1e-9 px of a rounding boundary (or not
-// finite) are recomputed with the reference's own division.
+// Reciprocal of z for the fast pixel path: the bare v_rcp_f64, accurate to 2^-24.4 relative
+// (measured over z in [1e-3, 1e3]: tools/gpu/rcp_probe.hip), so u = (x*fx)*rz + cx
+// lies within 1e3 * 2^-24.4 < 5e-5 px of the reference's (x*fx)/z + cx wherever a pixel can be
+// valid (|u - cx| < 1e3).  Steps whose u is within kPixMargin = 1e-4 px of a rounding boundary
+// (or not finite) are recomputed with the reference's own division (a Newton-refined reciprocal
+// with a 1e-9 px margin ran 2.6 % slower: the two FMAs cost more than the extra slow steps).
 // ---------------------------------------------------------------------------------------------
 // RN(a / b) given y = RN(1 / b): Markstein's correction step.  q0 = RN(a*y) is within 1 ulp
 // of a/b, r = a - b*q0 is exact with an FMA, and RN(q0 + r*y) is then the correctly rounded
@@ -398,9 +399,14 @@ __device__ inline float2 fma2(float2 a, float2 b, float2 c) {  // v_pk_fma_f32
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
-__device__ inline double refined_rcp(double z) {
-    const double y = __builtin_amdgcn_rcp(z);
-    return fma(y, fma(-z, y, 1.0), y);
+constexpr double kPixMargin = 1e-4;
+
+// v_cvt_i32_f64 clamps out-of-range inputs to INT_MIN / INT_MAX (a C cast would be undefined
+// there, so the instruction is named directly)
+__device__ inline int cvt_i32_sat(double x) {
+    int r;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(x));
+    return r;
 }
 
 __device__ inline double readlane_f64(double x, int l) {
@@ -493,7 +499,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         const double a2 = fma(fr.T[9], py, fr.T[8] * px);
         // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
         // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
-        // pixel lies within 1e-9 px of a rounding boundary are redone exactly afterwards.
+        // pixel lies within kPixMargin of a rounding boundary are redone exactly afterwards.
         double zc[NZ], uu[NZ], vv[NZ];
         unsigned inb = 0, slow = 0;
 #pragma unroll
@@ -502,13 +508,14 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-            const double rz = refined_rcp(z);
-            // one FMA for (x*fx)*rz + cx: within ~1e-11 px of the reference's (x*fx)/z + cx
-            // either way, far inside the 1e-9 px boundary margin below
+            const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see kPixMargin
+            // one FMA for (x*fx)*rz + cx: within 5e-5 px of the reference's (x*fx)/z + cx,
+            // inside the kPixMargin boundary margin below
             const double sx = fma(x * fr.fx, rz, fr.cx), sy = fma(y * fr.fy, rz, fr.cy);
             const double ux = rint(sx), uy = rint(sy);
-            // (a NaN fails both tests; far-out |s| may round differently but is invalid either way)
-            const bool ok = fabs(sx - ux) < 0.5 - 1e-9 && fabs(sy - uy) < 0.5 - 1e-9;
+            // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
+            // but is invalid either way)
+            const bool ok = fabs(sx - ux) < 0.5 - kPixMargin && fabs(sy - uy) < 0.5 - kPixMargin;
             const bool in = col_in && k < nz && z > 0.0;
             zc[k] = z;
             uu[k] = ux;
@@ -532,11 +539,13 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         const int W = fr.W, H = fr.H;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            const bool c = ((inb >> k) & 1u) && uu[k] >= 0.0 && uu[k] < (double)W &&
-                           vv[k] >= 0.0 && vv[k] < (double)H;
+            // saturating conversion, then unsigned bounds: out-of-range values clamp to INT_MIN /
+            // INT_MAX and fail.  uu, vv are integral and not NaN wherever z > 0: the exact path
+            // yields NaN only for a non-finite pose, whose z (np.linalg.inv: all NaN) fails z > 0
+            const int iu = cvt_i32_sat(uu[k]), iv = cvt_i32_sat(vv[k]);
+            const bool c = ((inb >> k) & 1u) && (unsigned)iu < (unsigned)W && (unsigned)iv < (unsigned)H;
             cand |= (unsigned)c << k;
-            // v*W + u is exact in f64; select before converting (no out-of-range conversion)
-            pix[k] = (int)(c ? fma(vv[k], (double)W, uu[k]) : 0.0);
+            pix[k] = c ? iv * W + iu : 0;
         }
         // phase 2: gather depth and colour for every step at once, before the depth test, so
         // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
