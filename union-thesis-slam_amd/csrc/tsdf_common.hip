@@ -203,7 +203,9 @@ int check_frame_args(const void* depth, int dk, const void* color, int ck, int H
     if (!depth || !color || !K || !Tinv) return set_error(TSDF_E_ARG, "null frame pointer");
     if (dk != TSDF_DEPTH_U16_MM && dk != TSDF_DEPTH_F64_M) return set_error(TSDF_E_ARG, "bad depth_kind %d", dk);
     if (ck != TSDF_COLOR_RGB8 && ck != TSDF_COLOR_F32) return set_error(TSDF_E_ARG, "bad color_kind %d", ck);
-    if (H <= 0 || W <= 0 || (long long)H * W >= (1ll << 31))
+    // < 2^28 pixels and sides < 2^24: the integrate's gathers use 32-bit byte offsets (8-byte f64
+    // depth texels) and a 24-bit multiply for v*W
+    if (H <= 0 || W <= 0 || H >= (1 << 24) || W >= (1 << 24) || (long long)H * W >= (1ll << 28))
         return set_error(TSDF_E_ARG, "bad image size %dx%d", H, W);
     return TSDF_OK;
 }

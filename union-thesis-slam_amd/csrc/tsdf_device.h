@@ -355,18 +355,24 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 // computed as q = m * 0.001 plus one FMA correction (exact for all 65536 inputs:
 // tools/check_depth_conversion.c).  depth_raw issues the u16 load; depth_m converts.  For f64
 // depth (DK == 1) depth_raw is unused and depth_m loads.
-template <int DK>
-__device__ inline unsigned depth_raw(const Frame& fr, int p) {
-    return DK == 0 ? (unsigned)((const unsigned short*)fr.depth)[p] : 0u;
+// p is a pixel index < 2^28 (check_frame_args), so byte offsets fit 32 bits: the loads take
+// the SGPR-base + 32-bit VGPR-offset form (no 64-bit address arithmetic per gather)
+template <typename T>
+__device__ inline T texel(const void* base, unsigned p) {
+    return *(const T*)((const char*)base + p * (unsigned)sizeof(T));
 }
 template <int DK>
-__device__ inline double depth_m(const Frame& fr, int p, unsigned raw) {
+__device__ inline unsigned depth_raw(const Frame& fr, unsigned p) {
+    return DK == 0 ? (unsigned)texel<unsigned short>(fr.depth, p) : 0u;
+}
+template <int DK>
+__device__ inline double depth_m(const Frame& fr, unsigned p, unsigned raw) {
     if (DK == 0) {
         const double m = (double)raw;
         const double q = m * 0.001;
         return fma(fma(-q, 1000.0, m), 0.001, q);
     }
-    return ((const double*)fr.depth)[p];
+    return texel<double>(fr.depth, p);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -480,7 +486,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     unsigned touched = 0;  // voxels updated by any frame of the batch (entry bits, hash)
     long long blk = -1;
     bool is_new = false;
-    int nupd = 0;
+    unsigned nupd = 0;  // this lane's voxel updates: one v_bcnt per frame (a per-step count, or a
+                        // wave-level ballot count, costs more VALU)
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
     bool c_canon = true;   // all loaded colours are canonical (canon_color)
 
@@ -535,7 +542,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             }
         }
         unsigned cand = 0;
-        int pix[NZ];
+        unsigned pix[NZ];
         const int W = fr.W, H = fr.H;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
@@ -545,7 +552,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const int iu = cvt_i32_sat(uu[k]), iv = cvt_i32_sat(vv[k]);
             const bool c = ((inb >> k) & 1u) && (unsigned)iu < (unsigned)W && (unsigned)iv < (unsigned)H;
             cand |= (unsigned)c << k;
-            pix[k] = c ? iv * W + iu : 0;
+            pix[k] = c ? __umul24((unsigned)iv, (unsigned)W) + (unsigned)iu : 0u;  // v_mad_u32_u24
         }
         // phase 2: gather depth and colour for every step at once, before the depth test, so
         // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
@@ -555,7 +562,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
             draw[k] = depth_raw<DK>(fr, pix[k]);
-            cpx[k] = (CK == 0) ? fr.rgbx[pix[k]] : __float_as_uint(((const float*)fr.color)[pix[k]]);
+            cpx[k] = texel<unsigned>(CK == 0 ? (const void*)fr.rgbx : fr.color, pix[k]);
         }
         __builtin_amdgcn_sched_barrier(0);
         double dep[NZ];
@@ -622,6 +629,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         loaded |= need;
         dirty |= need;
         touched |= vmask;
+        nupd += __popc(vmask);
         // phase 5: update in registers, straight-line; invalid steps keep their old values.
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
@@ -696,7 +704,6 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             ws[k] = ok ? wn : ws[k];
             ts[k] = ok ? tn : ts[k];
             cs[k] = ok ? cn : cs[k];
-            nupd += ok ? 1 : 0;
         }
     }
 #ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
