@@ -100,6 +100,28 @@ def test_ragged_and_degenerate_volumes(gf, bounds, vs):
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
 
 
+@pytest.mark.parametrize("cxy", [(1280.0, 960.0), (3000.5, -200.25)])
+def test_large_image_and_off_centre_principal_point(gf, cxy):
+    # 2560x1920 frames (the lounge frame upsampled 4x) with the principal point at the centre or
+    # outside the image: the fast pixel path's boundary margin scales with max(W, H) + |c|
+    # (frame_margin, csrc/tsdf_device.h), so the classification stays bit-exact
+    K = lounge_intrinsics().copy()
+    K[0, 0] *= 4.0
+    K[1, 1] *= 4.0
+    K[0, 2], K[1, 2] = cxy
+    vol = gf.TSDFVolume(np.array(C1), 0.04)
+    orc = O.OracleTSDFVolume(np.array(C1), 0.04)
+    for f in range(2):
+        _, depth, rgb, pose = load_lounge(f)
+        depth = np.ascontiguousarray(np.repeat(np.repeat(depth, 4, 0), 4, 1))
+        rgb = np.ascontiguousarray(np.repeat(np.repeat(rgb, 4, 0), 4, 1))
+        vol.integrate(rgb, depth, K, pose)
+        orc.integrate(rgb, depth, K, pose)
+    T, W, C = vol.get_state()
+    assert int((W > 0).sum()) > 0
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+
+
 def test_empty_and_invalid_depth_is_a_no_op(gf):
     K = lounge_intrinsics()
     vol = gf.TSDFVolume(np.array(C1), 0.04)

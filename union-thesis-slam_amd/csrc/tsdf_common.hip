@@ -313,6 +313,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->fy = (double)(float)K[4];
         fr->cx = (double)(float)K[2];
         fr->cy = (double)(float)K[5];
+        fr->half_m = 0.5 - frame_margin(W, H, fr->cx, fr->cy);
         fr->ow = ow ? ow[first + i] : ow_default;
         fr->ow32 = (float)fr->ow;
         fr->H = H;

@@ -48,6 +48,7 @@ struct Frame {
     double T[12];             // rows 0..2 of inv(cam_pose), row-major
     double fx, fy, cx, cy;    // f64(f32(K))  (cam2pix casts intr to float32, grid_fusion.py:190)
     double ow;                // obs_weight as a Python float (f64)
+    double half_m;            // 0.5 - the fast pixel path's boundary margin (frame_margin)
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
     const void* depth;        // depth read by cull/integrate: u16 millimetres or f64 metres
@@ -377,10 +378,9 @@ __device__ inline double depth_m(const Frame& fr, unsigned p, unsigned raw) {
 
 // ---------------------------------------------------------------------------------------------
 // Reciprocal of z for the fast pixel path: the bare v_rcp_f64, accurate to 2^-24.4 relative
-// (measured over z in [1e-3, 1e3]: tools/gpu/rcp_probe.hip), so u = (x*fx)*rz + cx
-// lies within 1e3 * 2^-24.4 < 5e-5 px of the reference's (x*fx)/z + cx wherever a pixel can be
-// valid (|u - cx| < 1e3).  Steps whose u is within kPixMargin = 1e-4 px of a rounding boundary
-// (or not finite) are recomputed with the reference's own division (a Newton-refined reciprocal
+// (random z in [1e-3, 1e3] and a 2^28-point mantissa sweep: tools/gpu/rcp_probe.hip), so
+// u = (x*fx)*rz + cx lies within |u - cx| * 2^-24.3 of the reference's (x*fx)/z + cx (< 3e-5 px
+// for 640x480).  Steps whose u is within frame_margin of a rounding boundary (or not finite) are recomputed with the reference's own division (a Newton-refined reciprocal
 // with a 1e-9 px margin ran 2.6 % slower: the two FMAs cost more than the extra slow steps).
 // ---------------------------------------------------------------------------------------------
 // RN(a / b) given y = RN(1 / b): Markstein's correction step.  q0 = RN(a*y) is within 1 ulp
@@ -405,7 +405,14 @@ __device__ inline float2 fma2(float2 a, float2 b, float2 c) {  // v_pk_fma_f32
     return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
 }
 
-constexpr double kPixMargin = 1e-4;
+// The fast path's pixel error is < |u - c| * 2^-24.3 (the bare reciprocal), and wherever the
+// boundary test matters |u - c| <= max(W, H) + max(|cx|, |cy|) -- a step closer than this margin to
+// a rounding boundary takes the exact path.  1e-4 px covers images up to ~1000 px; larger ones
+// scale it.  Host-side: stored per frame as half_m = 0.5 - margin.
+inline double frame_margin(int W, int H, double cx, double cy) {
+    const double span = (double)(W > H ? W : H) + fmax(fabs(cx), fabs(cy));
+    return fmax(1e-4, 1e-7 * span);
+}
 
 // v_cvt_i32_f64 clamps out-of-range inputs to INT_MIN / INT_MAX (a C cast would be undefined
 // there, so the instruction is named directly)
@@ -506,7 +513,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         const double a2 = fma(fr.T[9], py, fr.T[8] * px);
         // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
         // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
-        // pixel lies within kPixMargin of a rounding boundary are redone exactly afterwards.
+        // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
         double zc[NZ], uu[NZ], vv[NZ];
         unsigned inb = 0, slow = 0;
 #pragma unroll
@@ -515,14 +522,14 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-            const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see kPixMargin
-            // one FMA for (x*fx)*rz + cx: within 5e-5 px of the reference's (x*fx)/z + cx,
-            // inside the kPixMargin boundary margin below
+            const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see frame_margin
+            // one FMA for (x*fx)*rz + cx: within |u - cx| * 2^-24.3 of the reference's
+            // (x*fx)/z + cx, inside the frame_margin boundary margin below
             const double sx = fma(x * fr.fx, rz, fr.cx), sy = fma(y * fr.fy, rz, fr.cy);
             const double ux = rint(sx), uy = rint(sy);
             // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
             // but is invalid either way)
-            const bool ok = fabs(sx - ux) < 0.5 - kPixMargin && fabs(sy - uy) < 0.5 - kPixMargin;
+            const bool ok = fabs(sx - ux) < fr.half_m && fabs(sy - uy) < fr.half_m;
             const bool in = col_in && k < nz && z > 0.0;
             zc[k] = z;
             uu[k] = ux;
