@@ -103,7 +103,8 @@ int tsdf_dense_reset(tsdf_dense_t* h); /* tsdf = 1, weight = 0, colour = 0 (grid
 /* One frame: TSDFVolume.integrate(color_im, depth_im, cam_intr, cam_pose, obs_weight)
  * (grid_fusion.py:214-314).  K: the 3x3 intrinsics as given (row-major float64); the kernel uses
  * f64(f32(K)) like cam2pix (:190).  world_to_cam: np.linalg.inv(cam_pose) computed by the
- * caller (:265), row-major 4x4 float64. */
+ * caller (:265), row-major 4x4 float64.  Images: height, width < 2^24 and height*width < 2^28
+ * (the gathers use 32-bit byte offsets), else TSDF_E_ARG. */
 int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, const void* color,
                          int color_kind, int height, int width, const double K[9],
                          const double world_to_cam[16], double obs_weight, int flags);
