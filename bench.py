@@ -7,22 +7,26 @@
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-A step is one frame integrated (pyramid + fused cull/integrate kernels).  The F synthetic frames
-(tsdf_amd.scene: ray-cast room with spheres, u16 millimetre depth, RGB) are generated directly in
-HBM before timing; W warmup frames, then K timed frames issued as one asynchronous batch,
-bracketed by barrier + synchronize; the max over ranks is taken.  With N ranks each rank owns the
-8-voxel x-columns c with c % N == rank (cyclic column shards, DESIGN.md §6: balanced frustum
-share per rank) and integrates every frame into them -- no data-path collective -- so total work
-is fixed: "scaling": "strong".
+A step is one batch of 8 frames (the unit the kernels fuse: one three-stage k_fused launch
+integrates 8 frames with the brick state held in registers).  The F synthetic frames
+(tsdf_amd.scene: ray-cast room with spheres seen from the BENCH_RING trajectory, mean V_f 11.7 %
+of the volume; u16 millimetre depth, RGB) are generated directly in HBM before timing; W warmup
+steps, then K timed steps issued asynchronously, bracketed by barrier + synchronize; the max over
+ranks is taken.  With N ranks each rank owns the 8-voxel x-columns c with c % N == rank (cyclic
+column shards) and integrates every frame into them -- no data-path collective --
+so total work is fixed: "scaling": "strong".
 
 Rank 0 prints ONE JSON line.  `roofline` prices the integrate kernel by SURVEY §8(d)'s
 algorithmic bytes (24 B per updated voxel + 5 B per pixel per frame) over its HIP-event time;
-`cpu_baseline` is the C oracle (oracle/, scalar, one core) on a bounded sample of the same
-workload.
+`cpu_baseline` is the NumPy restatement of the reference's CPU path (oracle/, pinned to the
+reference fixtures) on a bounded sample, with the host's CPU model and BLAS threads.
+Beside `value`: the hash path, the PCIe-inclusive batch rate, the reference's own per-frame
+integrate() call pattern (`dropin`), and marching cubes of the fused volume.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -39,6 +43,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOM = 10.24
 VOXEL = 0.02
 PIX = 640 * 480
+BATCH = 8  # frames per step (kMaxBatch)
+WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) into 512^3 @ 2 cm dense grid"
+PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r02.json")
 
 
 def log(*a):
@@ -48,15 +55,17 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000, help="timed frames")
-    ap.add_argument("--warmup", type=int, default=100, help="untimed frames")
+    ap.add_argument("--steps", type=int, default=250, help="timed steps (batches of 8 frames)")
+    ap.add_argument("--warmup", type=int, default=12, help="untimed steps")
     ap.add_argument("--frames", type=int, default=1000, help="synthetic frames resident in HBM")
     ap.add_argument("--no-hash", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=5, help="CPU-baseline sample (~2 s per frame)")
+    ap.add_argument("--cpu-quick", action="store_true", help="CPU baseline without the 512^3 frame")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host-frame (PCIe) measurement")
     ap.add_argument("--ingest-frames", type=int, default=256)
+    ap.add_argument("--no-dropin", action="store_true", help="skip the per-frame integrate() measurement")
+    ap.add_argument("--dropin-frames", type=int, default=256)
     ap.add_argument("--no-mesh", action="store_true", help="skip the mesh-extraction measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: several ranks may share a GPU)")
@@ -75,8 +84,8 @@ def frame_ranges(start, count, F):
     return out
 
 
-def run_timed(vol, depth, rgb, K, Tinv, start, count, F, sync, barrier, profile):
-    """Issue `count` frames asynchronously; returns wall seconds (max over ranks)."""
+def run_timed(vol, depth, rgb, K, Tinv, start, count, F, sync, barrier, profile, async_=True):
+    """Issue `count` frames (asynchronously unless async_=False); returns wall seconds."""
     dptr, cptr = depth.data_ptr(), rgb.data_ptr()
     dstride, cstride = depth[0].numel() * 2, rgb[0].numel()
     hw = tuple(depth.shape[1:3])
@@ -87,11 +96,79 @@ def run_timed(vol, depth, rgb, K, Tinv, start, count, F, sync, barrier, profile)
     t0 = time.perf_counter()
     for s, n in frame_ranges(start, count, F):
         vol.integrate_batch(dptr + s * dstride, cptr + s * cstride, K, Tinv[s:s + n], hw=hw,
-                            device_ptrs=True, sync=False)
+                            device_ptrs=True, sync=not async_)
     vol.sync()
     sync()
-    dt = time.perf_counter() - t0
-    return dt
+    return time.perf_counter() - t0
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    blas = []
+    try:
+        from threadpoolctl import threadpool_info
+        blas = [{"api": d.get("internal_api"), "threads": d.get("num_threads")} for d in threadpool_info()
+                if d.get("user_api") == "blas"]
+    except Exception:
+        pass
+    return model, blas
+
+
+def cpu_baseline(depth, rgb, poses, K, first):
+    """The reference's CPU path restated in NumPy (oracle.numpy_port_integrate, the per-voxel
+    hash loop oracle.NumpyPortHash), pinned bit-exact to the reference fixtures by
+    tests/test_oracle_golden.py, timed on this host on a bounded sample."""
+    import oracle as O
+    model, blas = cpu_info()
+    threads = max([b["threads"] or 1 for b in blas] or [1])
+    res = {"unit": "frames/s", "kind": "port", "cpu_model": model, "host_cpus": os.cpu_count(),
+           "blas": blas, "cores": threads,
+           "cores_note": "NumPy elementwise passes run on one core; np.dot (rigid_transform) uses the "
+                         "BLAS threads listed"}
+    # config[0]: lounge frame 0 -> 128^3 @ 4 cm (SURVEY §8(d) C1), median of 7
+    d0, c0, p0, K0 = O.lounge_frame(0)
+    c1 = np.array([[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]])
+    vol = O.OracleTSDFVolume(c1.copy(), 0.04)
+    coords = O.vox_coords_for(vol._vol_dim)
+    ts = []
+    for _ in range(7):
+        vol = O.OracleTSDFVolume(c1.copy(), 0.04)
+        t0 = time.perf_counter()
+        n0 = O.numpy_port_integrate(vol, coords, c0, d0, K0, p0)
+        ts.append(time.perf_counter() - t0)
+    res["config0"] = {"s_per_frame_median": round(float(np.median(ts)), 4), "voxels_updated": n0,
+                      "sample": "lounge frame-000000 into 128^3 @ 4 cm, median of 7 (grid_fusion.py:214-314)"}
+    # hash: the per-voxel loop (hash_fusion.py:134-145) on the same frame
+    hp = O.NumpyPortHash(c1.copy(), 0.04, 1000000)
+    t0 = time.perf_counter()
+    nh = hp.integrate(coords, c0, d0, K0, p0)
+    th = time.perf_counter() - t0
+    res["hash_mvox_updates_per_s"] = round(nh / th / 1e6, 5)
+    res["hash_sample"] = f"lounge frame-000000 at 128^3 @ 4 cm: {nh} per-voxel updates in {th:.2f} s"
+    # the bench's own workload: one synthetic frame into the full 512^3 @ 2 cm volume
+    res["value"] = round(1.0 / float(np.median(ts)), 4)
+    res["sample"] = "config[0] only (--cpu-quick)"
+    if depth is not None:
+        big = O.OracleTSDFVolume(np.array([[0.0, ROOM]] * 3), VOXEL)
+        coords = O.vox_coords_for(big._vol_dim)
+        d = depth.astype(float) / 1000.0
+        t0 = time.perf_counter()
+        n = O.numpy_port_integrate(big, coords, rgb, d, K, poses)
+        tb = time.perf_counter() - t0
+        res["value"] = round(1.0 / tb, 5)
+        res["sample"] = (f"synthetic frame {first} into the full 512^3 @ 2 cm volume, {n} voxels updated, "
+                         f"{tb:.1f} s (vox_coords built untimed, as the reference's constructor does)")
+        res["mvox_updates_per_s"] = round(n / tb / 1e6, 3)
+        del coords, big
+    return res
 
 
 def main():
@@ -133,27 +210,26 @@ def main():
     def sync():
         torch.cuda.synchronize()
 
-    def max_over_ranks(x):
+    def reduce(x, op):
         if n == 1:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max_over_ranks(x):
+        return reduce(x, dist.ReduceOp.MAX if n > 1 else None)
+
     def sum_over_ranks(x):
-        if n == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+        return reduce(x, dist.ReduceOp.SUM if n > 1 else None)
 
     from tsdf_amd import _ffi, grid_fusion, hash_fusion, scene
 
     # ---- synthetic workload, generated in HBM ---------------------------------------------
     F = args.frames
     t0 = time.perf_counter()
-    poses = scene.trajectory(F, seed=0)
-    spheres = scene.make_spheres(0)
+    poses = scene.trajectory(F, seed=0, radius_frac=scene.BENCH_RING)
+    spheres = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
     depth = torch.empty((F, 480, 640), dtype=torch.int16, device=dev)
     rgb = torch.empty((F, 480, 640, 3), dtype=torch.uint8, device=dev)
     for s in range(0, F, 50):
@@ -165,43 +241,50 @@ def main():
     sync()
     log(f"[rank {rank}] generated {F} frames in HBM in {time.perf_counter() - t0:.1f}s")
 
-    # ---- dense grid: this rank's x-slab of 512^3 @ 2 cm --------------------------------------
+    # ---- dense grid: this rank's columns of 512^3 @ 2 cm ----------------------------------
     X = int(round(ROOM / VOXEL))
     bnds = np.array([[0.0, ROOM]] * 3)
-    import contextlib
     with contextlib.redirect_stdout(sys.stderr):  # the reference-style ctor prints; keep stdout JSON-only
         vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=gpu, shard=(rank, n))
-    W, Kt = args.warmup, args.steps
-    run_timed(vol, depth, rgb, K, Tinv, 0, W, F, sync, barrier, False)
-    dt = run_timed(vol, depth, rgb, K, Tinv, W, Kt, F, sync, barrier, not args.no_profile)
+    W, Ks = args.warmup, args.steps
+    Wf, Kf = W * BATCH, Ks * BATCH
+    run_timed(vol, depth, rgb, K, Tinv, 0, Wf, F, sync, barrier, False)
+    dt = run_timed(vol, depth, rgb, K, Tinv, Wf, Kf, F, sync, barrier, not args.no_profile)
     st = vol.stats()
     dt_max = max_over_ranks(dt)
     vox = sum_over_ranks(float(st["voxel_updates"]))
-    fps = Kt / dt_max
+    fps = Kf / dt_max
     kernel_s = st["kernel_ms"] / 1e3
     # roofline of the integrate kernel on this rank: algorithmic bytes / HIP-event time
-    alg_bytes = 24.0 * st["voxel_updates"] + 5.0 * PIX * Kt
+    alg_bytes = 24.0 * st["voxel_updates"] + 5.0 * PIX * Kf
     roof = None
     if st["kernel_launches"]:
+        avg_s = kernel_s / st["kernel_launches"]
         ach = alg_bytes / kernel_s / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "tsdf::k_fused<ow==1, NZ=4>: integrates batch k (and culls k+1, preps k+2 "
-                          "in the same launch); bytes = batch k's integrate bytes only",
-                "kernel_avg_us": round(1e6 * kernel_s / st["kernel_launches"], 2),
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "traffic_frac": None,
+                "kernel": "tsdf::k_fused<true, 4, 0>: integrates batch k (and culls k+1, preps k+2 in the "
+                          "same launch); bytes = batch k's integrate bytes only (SURVEY §8(d): 24 B per "
+                          "updated voxel + 5 B per pixel, x8 frames)",
+                "kernel_avg_us": round(1e6 * avg_s, 2),
                 "bytes_per_launch": round(alg_bytes / st["kernel_launches"]),
                 "launches": st["kernel_launches"]}
-        pmc = os.path.join(REPO, "profiles", "pmc_integrate_r01.json")
-        if os.path.exists(pmc):
-            with open(pmc) as fh:
+        if os.path.exists(PMC_PROFILE):
+            with open(PMC_PROFILE) as fh:
                 p = json.load(fh)
-            roof["traffic"] = p.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = "profiles/pmc_integrate_r01.json (separate rocprofv3 --pmc pass)"
-    vf_mean = st["voxel_updates"] / Kt
-    log(f"[rank {rank}] dense: {Kt} frames in {dt * 1e3:.1f} ms -> {Kt / dt:.0f} frames/s, "
+            if p.get("workload") == WORKLOAD and p.get("hbm_bytes_per_launch"):
+                tb = float(p["hbm_bytes_per_launch"])
+                roof["traffic"] = round(tb)
+                # measured DRAM-side bytes over this run's average launch time
+                roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+                roof["traffic_source"] = (os.path.relpath(PMC_PROFILE, REPO) + " (separate rocprofv3 --pmc "
+                                          "FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 rule)")
+    vf_mean = st["voxel_updates"] / Kf
+    log(f"[rank {rank}] dense: {Kf} frames in {dt * 1e3:.1f} ms -> {Kf / dt:.0f} frames/s, "
         f"V_f mean {vf_mean:.0f} ({100 * vf_mean / (len(vol.x_index) * X * X):.1f}% of shard), "
         f"kernel {st['kernel_ms']:.1f} ms over {st['kernel_launches']} launches, "
-        f"bricks visited/frame {st['bricks_visited'] / Kt:.0f}, touched/frame {st['bricks_touched'] / Kt:.0f}")
+        f"bricks visited/frame {st['bricks_visited'] / Kf:.0f}, touched/frame {st['bricks_touched'] / Kf:.0f}")
+    dense_bytes = 3 * 4 * len(vol.x_index) * X * X
     # ---- PCIe-inclusive rate: the same frames from pageable host memory (not `value`) -------
     ingest = None
     if not args.no_ingest:
@@ -222,81 +305,122 @@ def main():
         log(f"[rank {rank}] ingest: {ni} host frames in {ti * 1e3:.1f} ms -> {ni / ti:.0f} frames/s")
     # ---- mesh extraction of the fused volume (not part of `value`) ----
     mesh = None
-    if not args.no_mesh and rank == 0:
+    if not args.no_mesh and rank == 0 and n == 1:
         import ctypes
         nv, nt = ctypes.c_int64(), ctypes.c_int64()
         sync()
         t0 = time.perf_counter()
         _ffi.call("tsdf_dense_extract_mesh", vol._h, ctypes.byref(nv), ctypes.byref(nt))
         tm = time.perf_counter() - t0
-        nvox = len(vol.x_index) * X * X
         mesh = {"ms": round(1e3 * tm, 2), "vertices": nv.value, "triangles": nt.value,
-                "mvoxels_per_s": round(nvox / tm / 1e6, 1),
-                "note": "marching cubes on the device over the rank's shard after the timed run"}
+                "mvoxels_per_s": round(X ** 3 / tm / 1e6, 1),
+                "note": "marching cubes on the device over the fused 512^3 volume after the timed run"}
         log(f"[rank {rank}] mesh: {nv.value} vertices, {nt.value} triangles in {tm * 1e3:.1f} ms")
+    vol.close()
     del vol
     torch.cuda.empty_cache()
 
     # ---- voxel hash on the same frames (config[2]: 8^3 blocks, 2^22 buckets) ---------------
     hash_res = None
     if not args.no_hash:
-        nb = (X // 8) ** 3
         with contextlib.redirect_stdout(sys.stderr):
+            # pool sized for the live blocks, not the extent: it starts at 2^15 blocks and grows
+            # (synchronously in the warmup, ahead of the launches in the asynchronous timed run)
             ht = hash_fusion.HashTable(np.array([[0.0, ROOM]] * 3), VOXEL, 1 << 22, device=gpu,
-                                       max_blocks=nb, shard=rank, n_shards=n)
-        run_timed(ht, depth, rgb, K, Tinv, 0, W, F, sync, barrier, False)
-        hdt = run_timed(ht, depth, rgb, K, Tinv, W, Kt, F, sync, barrier, not args.no_profile)
+                                       max_blocks=1 << 15, shard=rank, n_shards=n)
+        run_timed(ht, depth, rgb, K, Tinv, 0, Wf, F, sync, barrier, False, async_=False)
+        hdt = run_timed(ht, depth, rgb, K, Tinv, Wf, Kf, F, sync, barrier, not args.no_profile)
         hs = ht.stats()
         info = ht.info()
         if hs["bricks_skipped"]:
             raise RuntimeError(f"hash table/pool overflowed ({hs['bricks_skipped']} bricks skipped)")
         hdt_max = max_over_ranks(hdt)
         hvox = sum_over_ranks(float(hs["voxel_updates"]))
-        hash_res = {"frames_per_s": round(Kt / hdt_max, 1),
+        used = sum_over_ranks(info["used"])
+        hash_bytes = info["capacity"] * (8 + 4) + info["pool_capacity"] * (3 * 4 * 512 + 64 + 4)
+        hash_res = {"frames_per_s": round(Kf / hdt_max, 1),
                     "mvox_updates_per_s": round(hvox / hdt_max / 1e6, 1),
-                    "ms_per_frame": round(1e3 * hdt_max / Kt, 4),
+                    "ms_per_step": round(1e3 * hdt_max / Ks, 4),
                     "buckets": 1 << 22, "block": "8^3",
-                    "load_factor": round(sum_over_ranks(info["used"]) / (1 << 22), 4),
-                    "blocks_live": int(sum_over_ranks(info["used"])),
+                    "load_factor": round(used / (1 << 22), 4),
+                    "blocks_live": int(used),
+                    "pool_capacity": int(sum_over_ranks(info["pool_capacity"])),
                     "mean_probe": round(hs["probe_steps"] / max(1, hs["lookups"]), 3),
                     "max_probe": int(hs["probe_max"]),
-                    "kernel_avg_us": round(1e3 * hs["kernel_ms"] / max(1, hs["kernel_launches"]), 2)}
-        log(f"[rank {rank}] hash: {Kt / hdt:.0f} frames/s, load {hash_res['load_factor']}")
+                    "kernel_avg_us": round(1e3 * hs["kernel_ms"] / max(1, hs["kernel_launches"]), 2),
+                    "hbm_state_bytes": int(sum_over_ranks(hash_bytes)),
+                    "dense_hbm_state_bytes": int(sum_over_ranks(dense_bytes)),
+                    "state_bytes_note": "hash: table keys + slot->block map + block pool (tsdf/weight/"
+                                        "colour, entry bits, free list) at its grown capacity; dense: "
+                                        "three f32 arrays of the volume"}
+        log(f"[rank {rank}] hash: {Kf / hdt:.0f} frames/s, load {hash_res['load_factor']}, "
+            f"pool {info['pool_capacity']} blocks for {info['used']} live")
+        ht.close()
         del ht
+        torch.cuda.empty_cache()
 
-    # ---- CPU baseline: the oracle (C, one core) on a bounded sample -------------------------
+    # ---- the reference's call pattern: one integrate() per host frame (drop-in) -------------
+    dropin = None
+    if not args.no_dropin and n == 1:
+        nd = min(args.dropin_frames, F)
+        d64 = depth[:nd].cpu().numpy().view(np.uint16).astype(np.float64) / 1000.0  # as grid_demo1.py:81
+        ch = rgb[:nd].cpu().numpy()
+        dropin = {"frames": nd, "call": "TSDFVolume.integrate(color_im u8, depth_im f64 m, K, pose) / "
+                                        "HashTable.integrate per frame from host numpy, then get_volume's "
+                                        "flush (grid_demo1.py:76-87, hash_demo1.py:39)"}
+        for name, mk in (("dense", lambda: grid_fusion.TSDFVolume(np.array([[0.0, ROOM]] * 3), VOXEL, device=gpu)),
+                         ("hash", lambda: hash_fusion.HashTable(np.array([[0.0, ROOM]] * 3), VOXEL, 1 << 22,
+                                                                device=gpu, max_blocks=1 << 15))):
+            with contextlib.redirect_stdout(sys.stderr):
+                v = mk()
+            v.integrate(ch[0], d64[0], K, poses[0])  # first call allocates the staging slots
+            v.sync()
+            t0 = time.perf_counter()
+            for i in range(1, nd):
+                v.integrate(ch[i], d64[i], K, poses[i])
+            v.sync()
+            td = time.perf_counter() - t0
+            dropin[name + "_frames_per_s"] = round((nd - 1) / td, 1)
+            v.close()
+            log(f"[rank {rank}] drop-in {name}: {(nd - 1) / td:.0f} frames/s per-frame integrate()")
+        with contextlib.redirect_stdout(sys.stderr):
+            v = grid_fusion.TSDFVolume(np.array([[0.0, ROOM]] * 3), VOXEL, device=gpu, defer=False)
+        nu = min(64, nd)
+        v.integrate(ch[0], d64[0], K, poses[0])
+        t0 = time.perf_counter()
+        for i in range(1, nu):
+            v.integrate(ch[i], d64[i], K, poses[i])
+        tu = time.perf_counter() - t0
+        dropin["dense_undeferred_frames_per_s"] = round((nu - 1) / tu, 1)
+        v.close()
+        del d64, ch
+        torch.cuda.empty_cache()
+
+    # ---- CPU baseline: the NumPy restatement of the reference CPU path --------------------
     cpu = None
     if rank == 0 and n == 1 and not args.no_cpu:
-        import oracle as O
-        nfr = max(1, args.cpu_frames)
-        ov = O.OracleTSDFVolume(np.array([[0.0, ROOM]] * 3), VOXEL)
-        dh = depth[W % F: W % F + nfr].cpu().numpy().view(np.uint16)
-        ch = rgb[W % F: W % F + nfr].cpu().numpy()
+        f0 = Wf % F
+        dh = None if args.cpu_quick else depth[f0].cpu().numpy().view(np.uint16)
+        ch = None if args.cpu_quick else rgb[f0].cpu().numpy()
         t0 = time.perf_counter()
-        for i in range(len(dh)):
-            ov.integrate(ch[i], dh[i].astype(float) / 1000.0, K, poses[W % F + i])
-        ct = time.perf_counter() - t0
-        cpu = {"value": round(len(dh) / ct, 4), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"{len(dh)} of the synthetic frames into the full 512^3 @ 2 cm volume "
-                         f"(oracle/tsdf_oracle.c, full-volume sweep like grid_fusion.py:260-314), "
-                         f"{ct:.1f} s",
-               "host_cpus": os.cpu_count()}
-        log(f"[rank 0] cpu oracle: {len(dh)} frames in {ct:.1f}s")
+        cpu = cpu_baseline(dh, ch, poses[f0], K, f0)
+        log(f"[rank 0] cpu baseline: {cpu['value']} frames/s ({time.perf_counter() - t0:.1f} s)")
 
     if rank == 0:
         line = {
             "metric": "depth frames/sec (640x480 into 512^3 @ 2 cm dense TSDF; hash alongside)",
-            "value": round(fps, 1), "unit": "frames/s", "n_gpus": n, "steps": Kt, "warmup": W,
-            "ms_per_step": round(1e3 * dt_max / Kt, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "value": round(fps, 1), "unit": "frames/s", "n_gpus": n, "steps": Ks, "warmup": W,
+            "ms_per_step": round(1e3 * dt_max / Ks, 4), "frames_per_step": BATCH,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (ray-cast 10.24 m room + spheres, u16 mm depth, RGB8; generated in HBM)",
-            "config": {"workload": "config[1]: 1000 synthetic 640x480 frames into 512^3 @ 2 cm dense grid",
-                       "volume": "512x512x512 @ 0.02 m", "frames_resident": F, "image": "640x480",
+            "config": {"workload": WORKLOAD, "volume": "512x512x512 @ 0.02 m", "frames_resident": F,
+                       "image": "640x480", "timed_frames": Kf,
                        "parallelism": f"cyclic 8-voxel x-columns over {n} ranks" if n > 1 else "single GPU"},
             "mvox_updates_per_s": round(vox / dt_max / 1e6, 1),
-            "mean_voxels_updated_per_frame": round(vox / Kt),
+            "mean_voxels_updated_per_frame": round(vox / Kf),
             "hash": hash_res,
             "pcie_inclusive": ingest,
+            "dropin": dropin,
             "mesh": mesh,
             "roofline": roof,
             "cpu_baseline": cpu,

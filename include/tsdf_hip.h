@@ -46,6 +46,11 @@ extern "C" {
 #define TSDF_ASYNC 2        /* do not synchronise the handle's stream before returning */
 #define TSDF_DEPTH_INVALID_65535 4 /* u16 depth: 65535 mm is invalid (0), the 7-Scenes convention
                                       of the demos (grid_demo1.py:82: depth_im[depth_im == 65.535] = 0) */
+#define TSDF_DEFER 8        /* tsdf_*_integrate (host frames only): copy the frame into a pinned
+                               staging batch and return; the batch runs (asynchronously, as one
+                               temporally batched launch) once it holds 8 frames or at the next
+                               other call on the handle -- the reference's one-integrate()-per-
+                               frame loop (grid_demo1.py:76-87) at batched speed, same results */
 
 typedef struct tsdf_dense tsdf_dense_t;
 typedef struct tsdf_hash tsdf_hash_t;

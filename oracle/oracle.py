@@ -10,10 +10,10 @@ Contents
   * ctypes front-end of tsdf_oracle.c (exact scalar restatement, see that file's header);
   * OracleTSDFVolume / OracleHashVolume: the reference's constructor semantics
     (grid_fusion.py:22-55, hash_fusion.py:34-69) around the C integrate;
-  * numpy_port_integrate: a vectorised NumPy restatement with the reference's own structure
+  * numpy_port_integrate / NumpyPortHash: NumPy restatements with the reference's own structure
     (full-volume vox2world -> np.dot rigid transform -> cam2pix -> masks -> gather/scatter,
-    grid_fusion.py:260-314) -- used as the timed CPU baseline, since it is what the
-    reference's CPU path costs;
+    grid_fusion.py:260-314; the per-voxel hash loop, hash_fusion.py:134-145) -- bench.py's timed
+    CPU baseline, pinned against the reference fixtures by tests/test_oracle_golden.py;
   * hash_keys: hash_function (hash_fusion.py:182-190) in int64 or wrapping-int32 mode.
 """
 from __future__ import annotations
@@ -172,15 +172,14 @@ def hash_keys(xyz, table_size: int, int_bits: int = 64) -> np.ndarray:
 
 
 # --------------------------------------------------------------------------------------------
-# NumPy port (timed CPU baseline).  Same structure and arithmetic as the reference CPU path;
+# NumPy port (bench.py's timed CPU baseline, pinned by tests/test_oracle_golden.py against the
+# reference-generated fixtures).  Same structure and arithmetic as the reference CPU path;
 # numba-typed helpers restated as vectorised NumPy with the casts numba would emit.
 # --------------------------------------------------------------------------------------------
 
-def numpy_port_integrate(vol: OracleTSDFVolume, vox_coords, color_im, depth_im, cam_intr,
-                         cam_pose, obs_weight=1.0):
-    """grid_fusion.py:225-314 restated; `vox_coords` is the (N,3) int meshgrid of :158-168."""
+def _numpy_project(vol, vox_coords, depth_im, cam_intr, cam_pose):
+    """grid_fusion.py:260-290 (hash_fusion.py:113-131): valid voxels, their distance and pixel."""
     im_h, im_w = depth_im.shape
-    color = fold_color(color_im)
     # vox2world (:170-181): f64 multiply-add, rounded once to f32
     o = vol._vol_origin.astype(np.float64)
     cam_pts = (o[None, :] + vol._voxel_size * vox_coords.astype(np.float32).astype(np.float64)
@@ -200,10 +199,17 @@ def numpy_port_integrate(vol: OracleTSDFVolume, vox_coords, color_im, depth_im, 
     depth_diff = depth_val - pix_z
     valid_pts = (depth_val > 0) & (depth_diff >= -vol._trunc_margin)
     dist = np.minimum(1, depth_diff / vol._trunc_margin)
+    return valid_pts, dist[valid_pts], pix_x[valid_pts], pix_y[valid_pts]
+
+
+def numpy_port_integrate(vol: OracleTSDFVolume, vox_coords, color_im, depth_im, cam_intr,
+                         cam_pose, obs_weight=1.0):
+    """grid_fusion.py:225-314 restated; `vox_coords` is the (N,3) int meshgrid of :158-168."""
+    color = fold_color(color_im)
+    valid_pts, valid_dist, px, py = _numpy_project(vol, vox_coords, depth_im, cam_intr, cam_pose)
     vx, vy, vz = (vox_coords[valid_pts, k] for k in range(3))
     w_old = vol._weight_vol_cpu[vx, vy, vz]
     tsdf_vals = vol._tsdf_vol_cpu[vx, vy, vz]
-    valid_dist = dist[valid_pts]
     # integrate_tsdf (:199-212) with numba's types
     w_new = (w_old.astype(np.float64) + obs_weight).astype(np.float32)
     t_new = (((w_old * tsdf_vals).astype(np.float64) + obs_weight * valid_dist)
@@ -215,7 +221,7 @@ def numpy_port_integrate(vol: OracleTSDFVolume, vox_coords, color_im, depth_im, 
     old_b = np.floor(old_color / 65536)
     old_g = np.floor((old_color - old_b * 65536) / 256)
     old_r = old_color - old_b * 65536 - old_g * 256
-    new_color = color[pix_y[valid_pts], pix_x[valid_pts]]
+    new_color = color[py, px]
     new_b = np.floor(new_color / 65536)
     new_g = np.floor((new_color - new_b * 65536) / 256)
     new_r = new_color - new_b * 65536 - new_g * 256
@@ -226,12 +232,79 @@ def numpy_port_integrate(vol: OracleTSDFVolume, vox_coords, color_im, depth_im, 
     return int(valid_pts.sum())
 
 
+class NumpyPortHash:
+    """HashTable's CPU integrate restated (hash_fusion.py:103-145): the vectorised projection,
+    then the reference's per-voxel Python loop -- get_hash_entry, and on a miss a new Voxel,
+    Voxel.integrate (data_structures/voxel.py:19-49, float64 state, np.round / np.minimum per
+    voxel) and add_hash_entry -- over the chained-bucket table of bucket_table.BucketTable.
+    obs_weight is not forwarded, as in the reference."""
+
+    def __init__(self, vol_bounds, voxel_size, map_size=1000000, int_bits=64):
+        from bucket_table import BucketTable
+        self._vol_bounds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
+            vol_bounds, voxel_size)
+        self._trunc_margin = 5 * self._voxel_size
+        self.table = BucketTable(map_size, int_bits)
+        self.sdf, self.weight, self.color = [], [], []  # per entry id (Voxel state)
+
+    def _voxel_integrate(self, e, new_dist, new_color, obs_weight=1.0):
+        w_old, d_old, c_old = self.weight[e], self.sdf[e], self.color[e]
+        w_new = w_old + obs_weight
+        self.sdf[e] = (d_old * w_old + new_dist * obs_weight) / w_new
+        self.weight[e] = w_new
+        old_b = np.floor(c_old / 65536)
+        old_g = np.floor((c_old - old_b * 65536) / 256)
+        old_r = c_old - old_b * 65536 - old_g * 256
+        new_b = np.floor(new_color / 65536)
+        new_g = np.floor((new_color - new_b * 65536) / 256)
+        new_r = new_color - new_b * 65536 - new_g * 256
+        bgr = np.minimum(255., np.round([(w_old * old_b + obs_weight * new_b) / w_new,
+                                         (w_old * old_g + obs_weight * new_g) / w_new,
+                                         (w_old * old_r + obs_weight * new_r) / w_new]))
+        self.color[e] = bgr[0] * 65536 + bgr[1] * 256 + bgr[2]
+
+    def integrate(self, vox_coords, color_im, depth_im, cam_intr, cam_pose, limit=None):
+        """One frame; `limit` stops after that many valid voxels (a bounded timing sample).
+        Returns the number of voxels integrated."""
+        color = fold_color(color_im)
+        valid_pts, valid_dist, px, py = _numpy_project(self, vox_coords, depth_im, cam_intr, cam_pose)
+        coords = vox_coords[valid_pts]
+        n = len(coords) if limit is None else min(limit, len(coords))
+        t = self.table
+        for i in range(n):
+            pos = coords[i]
+            e = t.get(pos)
+            if e is None:
+                e = len(t.pos)
+                self.sdf.append(1.0)
+                self.weight.append(0.0)
+                self.color.append(0.0)
+                self._voxel_integrate(e, valid_dist[i], color[py[i], px[i]])
+                t.add(pos)
+            else:
+                self._voxel_integrate(e, valid_dist[i], color[py[i], px[i]])
+        return n
+
+
 def vox_coords_for(dims) -> np.ndarray:
     """grid_fusion.py:158-168 (meshgrid ij, (N,3) int)."""
     xv, yv, zv = np.meshgrid(range(int(dims[0])), range(int(dims[1])), range(int(dims[2])),
                              indexing="ij")
     return np.concatenate([xv.reshape(1, -1), yv.reshape(1, -1), zv.reshape(1, -1)],
                           axis=0).astype(int).T
+
+
+def lounge_frame(i: int = 0):
+    """Lounge frame i from the committed fixture copy (tests/golden/lounge), ingested like
+    grid_demo1.py:80-84: depth u16 / 1000 with 65.535 -> 0, RGB, pose, intrinsics."""
+    from PIL import Image
+    root = os.path.join(os.path.dirname(_HERE), "tests", "golden", "lounge")
+    d = np.array(Image.open(os.path.join(root, "frame-%06d.depth.png" % i))).astype(float) / 1000.0
+    d[d == 65.535] = 0
+    rgb = np.array(Image.open(os.path.join(root, "frame-%06d.color.jpg" % i)).convert("RGB"))
+    pose = np.loadtxt(os.path.join(root, "frame-%06d.pose.txt" % i))
+    K = np.loadtxt(os.path.join(root, "camera-intrinsics.txt"), delimiter=" ")
+    return d, rgb, pose, K
 
 
 def view_frustum(max_depth: float, H: int, W: int, K, pose) -> np.ndarray:

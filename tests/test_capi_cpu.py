@@ -62,18 +62,19 @@ def test_argument_errors_are_reported_with_messages():
 
 
 def test_host_encoding_duties():
-    """Wrapper duties (SURVEY §8(b)): millimetre-exact depth goes as u16, anything else as f64;
-    uint8 colour goes as is, other colour is folded exactly like grid_fusion.py:228-232."""
+    """Wrapper duties: uint16 depth goes as millimetres, float depth as float64
+    metres untouched (the kernels read it as is); uint8 colour goes as is, other colour is folded
+    exactly like grid_fusion.py:228-232."""
     from tsdf_amd import _ffi
     from tsdf_amd.grid_fusion import encode_color, encode_depth, volume_geometry
     mm = np.array([[0, 1, 999, 65535]], np.uint16)
     d = mm.astype(float) / 1000.0
-    k, a = encode_depth(d)
+    k, a = encode_depth(mm)
     assert k == _ffi.DEPTH_U16_MM and np.array_equal(a, mm)
-    k, a = encode_depth(d + 1e-9)
-    assert k == _ffi.DEPTH_F64_M
-    k, a = encode_depth(-d)
-    assert k == _ffi.DEPTH_F64_M
+    k, a = encode_depth(d)
+    assert k == _ffi.DEPTH_F64_M and a is d  # no host pass, no copy
+    k, a = encode_depth(d.astype(np.float32))
+    assert k == _ffi.DEPTH_F64_M and a.dtype == np.float64
     rgb = np.arange(24, dtype=np.uint8).reshape(2, 4, 3)
     k, a = encode_color(rgb)
     assert k == _ffi.COLOR_RGB8 and a is not None

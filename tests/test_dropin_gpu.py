@@ -1,0 +1,120 @@
+"""The reference's call pattern through the drop-in wrappers: one integrate() per host frame
+(grid_demo1.py:76-87, hash_demo1.py:39), float64 metres as the demos pass them, deferred into
+batches of 8 frames on the device (TSDF_DEFER) -- bit-exact against the oracle whatever the
+flush points; and the asynchronous hash path's pool growth / overflow reporting.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+BNDS = [[0.0, 10.24]] * 3
+
+
+def _same(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
+
+
+def _synth(n, start=0):
+    from tsdf_amd import scene
+    poses = scene.trajectory(n, seed=0, start=start)
+    d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=start)
+    return np.ascontiguousarray(d.numpy()), np.ascontiguousarray(c.numpy()), poses
+
+
+def test_deferred_per_frame_integrate_matches_oracle():
+    """19 per-frame calls with f64 metres (half of them not millimetre-exact), varying
+    obs_weight, a change of intrinsics mid-stream and reads in between (each read runs the
+    pending frames first): deferred, undeferred and the oracle agree bit for bit."""
+    from tsdf_amd import grid_fusion
+    d, c, poses = _synth(19, start=333)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    K2 = K.copy()
+    K2[0, 0] = 590.0
+    rng = np.random.default_rng(3)
+    dv = grid_fusion.TSDFVolume(np.array(BNDS), 0.08)  # defer=True is the default
+    nv = grid_fusion.TSDFVolume(np.array(BNDS), 0.08, defer=False)
+    orc = O.OracleTSDFVolume(np.array(BNDS), 0.08)
+    n_orc = 0
+    for f in range(19):
+        m = d[f].astype(float) / 1000.0
+        if f % 2:
+            m = m + rng.uniform(0, 1e-5, size=m.shape) * (m > 0)
+        Kf = K2 if 9 <= f < 12 else K
+        ow = 1.0 if f % 5 else 0.5
+        for v in (dv, nv):
+            v.integrate(c[f], m, Kf, poses[f], obs_weight=ow)
+        n_orc += orc.integrate(c[f], m, Kf, poses[f], obs_weight=ow)
+        if f in (4, 13):
+            T, W, C = dv.get_state()
+            assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+    assert dv.stats()["voxel_updates"] == nv.stats()["voxel_updates"] == n_orc
+    for a, b, o in zip(dv.get_state(), nv.get_state(), (orc._tsdf_vol_cpu, orc._weight_vol_cpu, orc._color_vol_cpu)):
+        assert _same(a, o) and _same(b, o)
+
+
+def test_deferred_hash_per_frame_matches_dense():
+    """HashTable.integrate per frame (deferred, flushed synchronously so a full table / pool
+    grows and the skipped bricks re-run exactly) equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    d, c, poses = _synth(13, start=610)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.08, defer=False)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.08, 37, max_blocks=16)
+    for f in range(13):
+        m = d[f].astype(float) / 1000.0
+        g.integrate(c[f], m, K, poses[f])
+        h.integrate(c[f], m, K, poses[f])
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+    assert h.info()["capacity"] > 37 and h.info()["pool_capacity"] > 16
+
+
+def test_async_hash_overflow_is_reported_not_replayed():
+    """A pool far too small for asynchronous launches: the skipped bricks cannot be re-run (their
+    frames are gone), so the library reports TSDF_E_CAPACITY once, clears the overflow list (no
+    later call replays it against other frames), and the handle works again after reset()."""
+    from tsdf_amd import _ffi, grid_fusion, hash_fusion
+    d, c, poses = _synth(24, start=700)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.08, 1 << 12, max_blocks=64)
+    with pytest.raises(_ffi.TSDFError) as ei:
+        h.integrate_batch(d, c, K, Tinv, sync=False)
+        h.sync()
+    assert ei.value.code == _ffi.E_CAPACITY and "skipped" in str(ei.value)
+    assert h.stats()["bricks_skipped"] > 0
+    h.sync()  # reported once
+    h.reset()
+    h.integrate_batch(d, c, K, Tinv)  # synchronous: grows and re-runs exactly
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.08)
+    g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe):
+    """Asynchronous hash calls read each launch's pool report two launches later and grow the
+    pool / table before they fill: a continuing trajectory needs several growths and none of its
+    bricks is skipped; the result equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    monkeypatch.setenv("TSDF_PIPELINE", pipe)
+    d, c, poses = _synth(72, start=100)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.04, 1 << 12, max_blocks=256)  # 256^3: 8.2k blocks by the end
+    h.integrate_batch(d[:8], c[:8], K, Tinv[:8])  # synchronous start
+    cap0 = h.info()["pool_capacity"]
+    skipped0 = h.stats()["bricks_skipped"]
+    h.integrate_batch(d[8:], c[8:], K, Tinv[8:], sync=False)
+    h.sync()
+    assert h.stats()["bricks_skipped"] == skipped0
+    info = h.info()
+    assert info["pool_capacity"] > cap0 and info["capacity"] > 1 << 12
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.04)
+    g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)

@@ -187,3 +187,44 @@ def test_oracle_view_frustum_matches_reference_over_1000_frames():
     assert np.array_equal(b, g["bounds"])
     kat = np.array([[-4.22106438, 3.86798203], [-2.6663104, 2.60146141], [0., 5.76272371]])
     assert np.abs(b - kat).max() < 1e-8
+
+
+@pytest.mark.parametrize("name", ["dense_c1", "dense_c1_ow"])
+def test_numpy_port_matches_reference_fixture(name):
+    """bench.py's NumPy CPU baseline (oracle.numpy_port_integrate, the reference's own
+    full-volume structure) reproduces the reference fixture bit for bit."""
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    vol = O.OracleTSDFVolume(np.array([[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]]), 0.04)
+    coords = O.vox_coords_for(vol._vol_dim)
+    K = lounge_intrinsics()
+    for f in range(3):
+        _, depth, rgb, pose = load_lounge(f)
+        n = O.numpy_port_integrate(vol, coords, rgb, depth, K, pose, obs_weight=float(g["obs_weight"][f]))
+        assert n == int(g["f%d_nupd" % f])
+        idx, t, w, c = _state(vol)
+        assert np.array_equal(idx, g["f%d_idx" % f])
+        assert np.array_equal(t.view(np.uint32), g["f%d_tsdf" % f].view(np.uint32))
+        assert np.array_equal(w, g["f%d_weight" % f]) and np.array_equal(c, g["f%d_color" % f])
+
+
+@pytest.mark.slow
+def test_numpy_port_hash_matches_reference_hash_path():
+    """bench.py's hash CPU baseline (oracle.NumpyPortHash: the per-voxel loop of
+    hash_fusion.py:134-145 over the chained-bucket table, float64 Voxel state) reproduces the
+    reference's hash fixture exactly, table statistics included."""
+    g = np.load(os.path.join(GOLD, "hash_c1.npz"))
+    hp = O.NumpyPortHash(np.array([[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]]), 0.04, 1000000)
+    coords = O.vox_coords_for(hp._vol_dim)
+    K = lounge_intrinsics()
+    for f in range(3):
+        _, depth, rgb, pose = load_lounge(f)
+        hp.integrate(coords, rgb, depth, K, pose)
+        t = hp.table
+        pos = np.array(t.pos, np.int64)
+        order = np.lexsort((pos[:, 2], pos[:, 1], pos[:, 0]))
+        assert np.array_equal(pos[order], g["f%d_pos" % f])
+        assert np.array_equal(np.array(hp.sdf)[order], g["f%d_sdf" % f])
+        assert np.array_equal(np.array(hp.weight)[order], g["f%d_weight" % f])
+        assert np.array_equal(np.array(hp.color)[order], g["f%d_color" % f])
+        assert t.count_entries() == int(g["f%d_entries" % f])
+        assert t.nonempty == int(g["f%d_nonempty" % f]) and t.collisions() == int(g["f%d_collisions" % f])

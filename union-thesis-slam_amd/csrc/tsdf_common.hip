@@ -261,29 +261,15 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
     const char* d = (const char*)depth + dbytes * (size_t)first;
     const char* c = (const char*)color + cbytes * (size_t)first;
     if (!(flags & TSDF_DEVICE_PTRS)) {  // stage the batch's frames into staging slot `slot`
-        if (st_depth_bytes < dbytes * kMaxBatch || st_color_bytes < cbytes * kMaxBatch) {
-            TSDF_TRY(sync_all());
-            for (int k = 0; k < kSlots; ++k) {
-                if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
-                if (st_color[k]) TSDF_HIP(hipFree(st_color[k]));
-                if (hst_depth[k]) TSDF_HIP(hipHostFree(hst_depth[k]));
-                if (hst_color[k]) TSDF_HIP(hipHostFree(hst_color[k]));
-                st_depth[k] = st_color[k] = hst_depth[k] = hst_color[k] = nullptr;
-            }
-            st_depth_bytes = st_color_bytes = 0;
-            for (int k = 0; k < kSlots; ++k) {
-                TSDF_HIP(hipMalloc(&st_depth[k], dbytes * kMaxBatch));
-                TSDF_HIP(hipMalloc(&st_color[k], cbytes * kMaxBatch));
-                TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * kMaxBatch, hipHostMallocDefault));
-                TSDF_HIP(hipHostMalloc(&hst_color[k], cbytes * kMaxBatch, hipHostMallocDefault));
-            }
-            st_depth_bytes = dbytes * kMaxBatch;
-            st_color_bytes = cbytes * kMaxBatch;
+        if (prestaged >= 0) {  // deferred frames: already copied into bounce slot `prestaged`
+            slot = prestaged;
+        } else {
+            TSDF_TRY(stage_alloc(dbytes, cbytes));
+            // the bounce slot is free once its previous DMA has finished
+            TSDF_HIP(hipEventSynchronize(ev_copied[slot]));
+            par_memcpy(hst_depth[slot], d, dbytes * n);
+            par_memcpy(hst_color[slot], c, cbytes * n);
         }
-        // the bounce slot is free once its previous DMA has finished
-        TSDF_HIP(hipEventSynchronize(ev_copied[slot]));
-        par_memcpy(hst_depth[slot], d, dbytes * n);
-        par_memcpy(hst_color[slot], c, cbytes * n);
         TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[slot], 0));
         TSDF_HIP(hipMemcpyAsync(st_depth[slot], hst_depth[slot], dbytes * n, hipMemcpyHostToDevice, cstream));
         TSDF_HIP(hipMemcpyAsync(st_color[slot], hst_color[slot], cbytes * n, hipMemcpyHostToDevice, cstream));
@@ -335,12 +321,62 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
     return TSDF_OK;
 }
 
+int Base::stage_alloc(size_t dbytes, size_t cbytes) {
+    if (st_depth_bytes >= dbytes * kMaxBatch && st_color_bytes >= cbytes * kMaxBatch) return TSDF_OK;
+    TSDF_TRY(sync_all());
+    for (int k = 0; k < kSlots; ++k) {
+        if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
+        if (st_color[k]) TSDF_HIP(hipFree(st_color[k]));
+        if (hst_depth[k]) TSDF_HIP(hipHostFree(hst_depth[k]));
+        if (hst_color[k]) TSDF_HIP(hipHostFree(hst_color[k]));
+        st_depth[k] = st_color[k] = hst_depth[k] = hst_color[k] = nullptr;
+    }
+    st_depth_bytes = st_color_bytes = 0;
+    for (int k = 0; k < kSlots; ++k) {
+        TSDF_HIP(hipMalloc(&st_depth[k], dbytes * kMaxBatch));
+        TSDF_HIP(hipMalloc(&st_color[k], cbytes * kMaxBatch));
+        TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * kMaxBatch, hipHostMallocDefault));
+        TSDF_HIP(hipHostMalloc(&hst_color[k], cbytes * kMaxBatch, hipHostMallocDefault));
+    }
+    st_depth_bytes = dbytes * kMaxBatch;
+    st_color_bytes = cbytes * kMaxBatch;
+    return TSDF_OK;
+}
+
+bool Base::defer_same(int dk, int ck, int H, int W, const double* K) const {
+    return dfr.dk == dk && dfr.ck == ck && dfr.H == H && dfr.W == W && std::memcmp(dfr.K, K, sizeof(dfr.K)) == 0;
+}
+
+int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H, int W,
+                     const double* K, const double* T, double ow) {
+    const size_t dbytes = frame_bytes_depth(dk, H, W), cbytes = frame_bytes_color(ck, H, W);
+    if (dfr.n == 0) {
+        TSDF_TRY(stage_alloc(dbytes, cbytes));
+        dfr.slot = defer_next;
+        defer_next = (defer_next + 1) % kSlots;
+        TSDF_HIP(hipEventSynchronize(ev_copied[dfr.slot]));  // its previous DMA has finished
+        dfr.dk = dk;
+        dfr.ck = ck;
+        dfr.H = H;
+        dfr.W = W;
+        std::memcpy(dfr.K, K, sizeof(dfr.K));
+    }
+    const int i = dfr.n;
+    par_memcpy((char*)hst_depth[dfr.slot] + dbytes * i, depth, dbytes);
+    par_memcpy((char*)hst_color[dfr.slot] + cbytes * i, color, cbytes);
+    std::memcpy(dfr.T + 16 * i, T, 16 * sizeof(double));
+    dfr.ow[i] = ow;
+    dfr.n = i + 1;
+    return TSDF_OK;
+}
+
 int Base::begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags) {
     (void)depth, (void)dbytes, (void)color, (void)cbytes, (void)flags;
     return TSDF_OK;
 }
 
 int Base::end_batch(int flags, int slot) {
+    if (prestaged >= 0) slot = prestaged;
     if (!(flags & TSDF_DEVICE_PTRS)) TSDF_HIP(hipEventRecord(ev_free[slot], stream));
     return TSDF_OK;
 }
@@ -352,12 +388,15 @@ int Base::end_call(int flags) {
 
 int Base::launch_prep(const Batch& bt, int dk, int ck, int W, int H, hipStream_t stream) {
     dim3 grid((W + 63) / 64, (H + 63) / 64, bt.n);
-    bool vec = dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0;
-    for (int i = 0; i < bt.n && vec; ++i)  // 8-byte depth, 4-byte colour, 16-byte RGBX rows
-        vec = ((uintptr_t)bt.f[i].depth_src % 8 == 0) && ((uintptr_t)bt.f[i].color % 4 == 0) &&
+    bool vec = ck == TSDF_COLOR_RGB8 && W % 4 == 0;
+    const unsigned dal = dk == TSDF_DEPTH_U16_MM ? 8u : 16u;
+    for (int i = 0; i < bt.n && vec; ++i)  // 8/16-byte depth, 4-byte colour, 16-byte RGBX rows
+        vec = ((uintptr_t)bt.f[i].depth_src % dal == 0) && ((uintptr_t)bt.f[i].color % 4 == 0) &&
               ((uintptr_t)bt.f[i].rgbx % 16 == 0) && ((uintptr_t)bt.f[i].depth_mask % 8 == 0);
-    if (vec)
+    if (vec && dk == TSDF_DEPTH_U16_MM)
         hipLaunchKernelGGL(k_prep_vec<0>, grid, dim3(512), 0, stream, bt, count);
+    else if (vec)
+        hipLaunchKernelGGL(k_prep_vec<1>, grid, dim3(512), 0, stream, bt, count);
     else if (dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8)
         hipLaunchKernelGGL((k_prep<0, 0>), grid, dim3(1024), 0, stream, bt, count);
     else if (dk == TSDF_DEPTH_U16_MM)

@@ -104,8 +104,8 @@ int dense_run_inline(tsdf_dense* h, int n_frames, const void* depth, int dk, con
 // The fused path (k_fused, tsdf_device.h): launch L runs integrate(L), cull(L+1) and prep(L+2)
 // of the call's batches, L = -2 .. nb-1.  Batch j uses buffer set and staging slot j % kSets.
 // u16 depth + RGB8 with the vectorised prep's alignment only (the bench's and the demos' case).
-int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, const void* color, int H, int W,
-                    const double* K, const double* Tinv, const double* ow, int flags) {
+int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, const void* color, int H,
+                    int W, const double* K, const double* Tinv, const double* ow, int flags) {
     Base& B = h->b;
     TSDF_TRY(B.use_sets(kSets));
     const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
@@ -119,7 +119,7 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, const void* 
             const int f0 = jp * kMaxBatch;
             const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
             B.use_set(jp % kSets);
-            TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, TSDF_DEPTH_U16_MM, color, TSDF_COLOR_RGB8, H, W,
+            TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, dk, color, TSDF_COLOR_RGB8, H, W,
                                      K, Tinv, ow, 1.0, flags, f0, n, jp % kSlots));
         }
         const bool has_i = L >= 0, has_c = L + 1 >= 0 && L + 1 < nb, has_p = jp < nb;
@@ -147,17 +147,21 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, const void* 
         for (int i = 0; i < bi.n; ++i) ow1 = ow1 && bi.f[i].ow == 1.0;
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
-        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0);
+        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0) | (dk == TSDF_DEPTH_U16_MM ? 0 : 4);
         switch (sel) {
-#define TSDF_LAUNCH(S, OW_, NZ_)                                                                        \
+#define TSDF_LAUNCH(S, OW_, NZ_, DK_)                                                                   \
     case S:                                                                                             \
-        hipLaunchKernelGGL((k_fused<OW_, NZ_>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, \
-                           bc, bp, B.pool, B.stats, sg);                                                \
+        hipLaunchKernelGGL((k_fused<OW_, NZ_, DK_>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, \
+                           bi, bc, bp, B.pool, B.stats, sg);                                            \
         break;
-            TSDF_LAUNCH(0, false, 8)
-            TSDF_LAUNCH(1, true, 8)
-            TSDF_LAUNCH(2, false, 4)
-            TSDF_LAUNCH(3, true, 4)
+            TSDF_LAUNCH(0, false, 8, 0)
+            TSDF_LAUNCH(1, true, 8, 0)
+            TSDF_LAUNCH(2, false, 4, 0)
+            TSDF_LAUNCH(3, true, 4, 0)
+            TSDF_LAUNCH(4, false, 8, 1)
+            TSDF_LAUNCH(5, true, 8, 1)
+            TSDF_LAUNCH(6, false, 4, 1)
+            TSDF_LAUNCH(7, true, 4, 1)
 #undef TSDF_LAUNCH
         }
         TSDF_HIP(hipGetLastError());
@@ -177,20 +181,36 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
-    // the fused pipeline needs the vectorised prep: u16 + RGB8, W % 4 == 0 and (device frames)
-    // 8-byte depth / 4-byte colour alignment of every frame (host frames are staged aligned)
-    bool fused = h->fused && dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
+    // the fused pipeline needs the vectorised prep: u16 or f64 depth + RGB8, W % 4 == 0 and
+    // (device frames) 8-byte u16 / 16-byte f64 depth and 4-byte colour alignment of every frame
+    // (host frames are staged aligned)
+    bool fused = h->fused && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
     if (fused && (flags & TSDF_DEVICE_PTRS))
-        fused = (uintptr_t)depth % 8 == 0 && (uintptr_t)color % 4 == 0 && ((size_t)H * W) % 4 == 0;
-    if (fused) TSDF_TRY(dense_run_fused(h, n_frames, depth, color, H, W, K, Tinv, ow, flags));
+        fused = (uintptr_t)depth % (dk == TSDF_DEPTH_U16_MM ? 8 : 16) == 0 && (uintptr_t)color % 4 == 0 &&
+                ((size_t)H * W) % 4 == 0;
+    if (fused) TSDF_TRY(dense_run_fused(h, n_frames, depth, dk, color, H, W, K, Tinv, ow, flags));
     else TSDF_TRY(dense_run_inline(h, n_frames, depth, dk, color, ck, H, W, K, Tinv, ow, flags));
     TSDF_TRY(guard.finish());
     if (!(flags & TSDF_ASYNC)) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;
 }
 
+// Run the deferred frames (TSDF_DEFER) as one asynchronous batch from their bounce slot.
+int dense_flush(tsdf_dense* h) {
+    Base& B = h->b;
+    if (B.dfr.n == 0) return TSDF_OK;
+    const Base::Deferred d = B.dfr;
+    B.dfr.n = 0;
+    B.prestaged = d.slot;
+    const int r = dense_run(h, d.n, B.hst_depth[d.slot], d.dk, B.hst_color[d.slot], d.ck, d.H, d.W, d.K, d.T,
+                            d.ow, TSDF_ASYNC);
+    B.prestaged = -1;
+    return r;
+}
+
 int dense_xfer(tsdf_dense* h, float* tsdf_, float* weight_, float* color_, bool get) {
     Base& B = h->b;
+    TSDF_TRY(dense_flush(h));
     TSDF_HIP(hipSetDevice(B.device));
     const size_t n = (size_t)B.vol.dims[0] * B.vol.dims[1] * B.vol.dims[2];
     float* tmp = nullptr;
@@ -301,6 +321,7 @@ int tsdf_dense_destroy(tsdf_dense_t* h) {
 int tsdf_dense_reset(tsdf_dense_t* h) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     Base& B = h->b;
+    B.dfr.n = 0;  // deferred frames are dropped with the state
     TSDF_HIP(hipSetDevice(B.device));
     hipLaunchKernelGGL(k_fill3, dim3(4096), dim3(256), 0, B.stream, B.pool.tsdf, B.pool.weight,
                        B.pool.color, (size_t)B.n_bricks * kBrickVox);
@@ -316,6 +337,16 @@ int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, con
                          const double world_to_cam[16], double obs_weight, int flags) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    TSDF_HIP(hipSetDevice(h->b.device));
+    Base& B = h->b;
+    if (flags & TSDF_DEFER) {
+        if (flags & TSDF_DEVICE_PTRS) return set_error(TSDF_E_ARG, "TSDF_DEFER takes host frames only");
+        if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(dense_flush(h));
+        TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, obs_weight));
+        if (B.dfr.n == kMaxBatch) TSDF_TRY(dense_flush(h));
+        return TSDF_OK;
+    }
+    TSDF_TRY(dense_flush(h));
     return dense_run(h, 1, depth, depth_kind, color, color_kind, height, width, K, world_to_cam,
                      &obs_weight, flags);
 }
@@ -328,6 +359,8 @@ int tsdf_dense_integrate_batch(tsdf_dense_t* h, int n_frames, const void* depth,
     if (n_frames < 0) return set_error(TSDF_E_ARG, "n_frames < 0");
     if (n_frames == 0) return TSDF_OK;
     TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(dense_flush(h));
     return dense_run(h, n_frames, depth, depth_kind, color, color_kind, height, width, K,
                      world_to_cam, obs_weight, flags);
 }
@@ -345,6 +378,7 @@ int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf_, const float* weight_, co
 int tsdf_dense_sync(tsdf_dense_t* h) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(dense_flush(h));
     TSDF_HIP(hipStreamSynchronize(h->b.stream));
     return TSDF_OK;
 }
@@ -352,12 +386,14 @@ int tsdf_dense_sync(tsdf_dense_t* h) {
 int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(dense_flush(h));
     return h->b.read_stats(out, reset);
 }
 
 int tsdf_dense_extract_mesh(tsdf_dense_t* h, int64_t* n_verts, int64_t* n_tris) {
     if (!h || !n_verts || !n_tris) return set_error(TSDF_E_ARG, "null pointer");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(dense_flush(h));
     TSDF_TRY(extract_mesh(h->b, h->b.pool, h->mesh));
     *n_verts = h->mesh.n_verts;
     *n_tris = h->mesh.n_tris;
@@ -373,6 +409,7 @@ int tsdf_dense_get_mesh(tsdf_dense_t* h, float* verts, float* normals, uint8_t* 
 int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(dense_flush(h));
     return h->b.set_profiling(on);
 }
 

@@ -113,6 +113,16 @@ struct PoolState {
     long long n_overflow;  // bricks skipped for lack of space (re-run after growing)
 };
 
+// Pool state after launch `seq`, written by the committing thread into page-locked host memory
+// (slot seq % kReports; `seq` stored last, system scope): asynchronous hash calls read it a
+// couple of launches later to grow the pool / table before they fill up, and to detect
+// skipped bricks, without a stream synchronisation per batch.
+constexpr int kReports = 8;
+struct PoolReport {
+    long long pool_top, free_count, n_overflow;
+    long long seq;  // launch number + 1 (0: slot never written)
+};
+
 struct Table {
     unsigned long long* keys;   // capacity slots; kEmpty / kTomb / packed brick key
     int* vals;                  // pool block of each slot
@@ -120,6 +130,7 @@ struct Table {
     int* free_list;
     ListEntry* overflow;        // list entries skipped this launch
     PoolState* st;
+    PoolReport* rb;             // kReports host-mapped report slots (nullptr: none)
     long long capacity;
     long long shard_cap;        // capacity at create: bucket-range ownership stays fixed across resizes
     long long max_blocks;
@@ -916,10 +927,12 @@ __device__ inline void pyr_level(const PyrGeo& pg, float* pyr, int L, const floa
     }
 }
 
-// k_prep for u16 depth + RGB8 with W % 4 == 0 and aligned buffers (the common case): 512 threads
-// per 64x64 tile, 4x2 pixels per thread, moved with 8-byte depth loads, three 4-byte colour loads
-// per row (4 packed RGB pixels) and one 16-byte RGBX store per row -- instead of one 2-byte and
-// three 1-byte loads and one 4-byte store per pixel.  Same outputs as k_prep<0, 0>.
+// k_prep for u16 (DK = 0) or f64 (DK = 1) depth + RGB8 with W % 4 == 0 and aligned buffers (the
+// common case): 512 threads per 64x64 tile, 4x2 pixels per thread, moved with 8-byte u16 depth
+// loads (two 16-byte loads for f64), three 4-byte colour loads per row (4 packed RGB pixels) and
+// one 16-byte RGBX store per row -- instead of one 2-byte and three 1-byte loads and one 4-byte
+// store per pixel.  Same outputs as k_prep<DK, 0>.
+template <int DK = 0>
 __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int tx, int ty, int tf,
                                      float (*sa)[33], float (*sb)[33]) {
     const Frame& fr = bt.f[tf];
@@ -934,18 +947,25 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
             const int y = y0 + dy;
             if (y >= fr.H) continue;
             const size_t p = (size_t)y * fr.W + x0;
-            uint2 dd = *(const uint2*)((const unsigned short*)fr.depth_src + p);
-            if (fr.depth_mask) {  // the demos' depth_im[depth_im == 65.535] = 0
-                unsigned lo0 = dd.x & 0xFFFFu, hi0 = dd.x >> 16, lo1 = dd.y & 0xFFFFu, hi1 = dd.y >> 16;
-                lo0 = lo0 == 65535u ? 0u : lo0;
-                hi0 = hi0 == 65535u ? 0u : hi0;
-                lo1 = lo1 == 65535u ? 0u : lo1;
-                hi1 = hi1 == 65535u ? 0u : hi1;
-                dd = make_uint2(lo0 | (hi0 << 16), lo1 | (hi1 << 16));
-                *(uint2*)(fr.depth_mask + p) = dd;
+            if (DK == 1) {  // f64 metres (the reference's own depth_im)
+                const double2 d0 = *(const double2*)((const double*)fr.depth_src + p);
+                const double2 d1 = *(const double2*)((const double*)fr.depth_src + p + 2);
+                ma = fmaxf(ma, fmaxf((float)d0.x, (float)d0.y));
+                mb = fmaxf(mb, fmaxf((float)d1.x, (float)d1.y));
+            } else {
+                uint2 dd = *(const uint2*)((const unsigned short*)fr.depth_src + p);
+                if (fr.depth_mask) {  // the demos' depth_im[depth_im == 65.535] = 0
+                    unsigned lo0 = dd.x & 0xFFFFu, hi0 = dd.x >> 16, lo1 = dd.y & 0xFFFFu, hi1 = dd.y >> 16;
+                    lo0 = lo0 == 65535u ? 0u : lo0;
+                    hi0 = hi0 == 65535u ? 0u : hi0;
+                    lo1 = lo1 == 65535u ? 0u : lo1;
+                    hi1 = hi1 == 65535u ? 0u : hi1;
+                    dd = make_uint2(lo0 | (hi0 << 16), lo1 | (hi1 << 16));
+                    *(uint2*)(fr.depth_mask + p) = dd;
+                }
+                ma = fmaxf(ma, fmaxf((float)(dd.x & 0xFFFFu) * 1e-3f, (float)(dd.x >> 16) * 1e-3f));
+                mb = fmaxf(mb, fmaxf((float)(dd.y & 0xFFFFu) * 1e-3f, (float)(dd.y >> 16) * 1e-3f));
             }
-            ma = fmaxf(ma, fmaxf((float)(dd.x & 0xFFFFu) * 1e-3f, (float)(dd.x >> 16) * 1e-3f));
-            mb = fmaxf(mb, fmaxf((float)(dd.y & 0xFFFFu) * 1e-3f, (float)(dd.y >> 16) * 1e-3f));
             const unsigned* q = (const unsigned*)((const unsigned char*)fr.color + 3 * p);
             const unsigned a = q[0], b = q[1], cc = q[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
             *(uint4*)((unsigned*)fr.rgbx + p) =
@@ -974,11 +994,11 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
     pyr_level<0>(bt.pg, pyr, 6, sa, sb, 1, tx, ty);
 }
 
-template <int = 0>
+template <int DK = 0>
 __global__ __launch_bounds__(512) void k_prep_vec(Batch bt, unsigned int* count) {
     __shared__ float sa[32][33];
     __shared__ float sb[32][33];
-    prep_vec_tile(bt, count, blockIdx.x, blockIdx.y, blockIdx.z, sa, sb);
+    prep_vec_tile<DK>(bt, count, blockIdx.x, blockIdx.y, blockIdx.z, sa, sb);
 }
 
 template <int DK, int CK>
@@ -1054,9 +1074,10 @@ struct Stage {
     unsigned int* count_p;   // prep: count of batch k+2 (reset for its cull)
     int gi, gc;              // integrate / cull workgroups
     int ptx, pty;            // prep tiles per frame (x, y)
+    long long seq;           // hash: launch number for the pool report (Table::rb)
 };
 
-template <bool OW1, int NZ>
+template <bool OW1, int NZ, int DK = 0>
 __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_DENSE_WAVES))) void k_fused(Vol v, Batch bi, Batch bc, Batch bp,
                                                                      Pool pool, unsigned long long* stats,
                                                                      Stage sg) {
@@ -1071,7 +1092,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
             for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedWG / 64;
-        integrate_list<false, 0, 0, OW1, NZ>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
+        integrate_list<false, DK, 0, OW1, NZ>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
                                              OW1 ? s_buf : nullptr);
         __syncthreads();
@@ -1083,27 +1104,36 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;
         float(*sa)[33] = (float(*)[33])s_buf;
-        prep_vec_tile(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
+        prep_vec_tile<DK>(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
     }
 }
 
 // Fold one launch's allocations (PoolState::cursor) into the free list / bump pointer (the
 // hash's k_commit, also run by the last integrate workgroup of a fused hash launch).
-__device__ inline void commit_pool(PoolState* st, long long max_blocks) {
+__device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolReport* rb = nullptr,
+                                   long long seq = -1) {
     const long long used = coh_load(&st->cursor);
     const long long nf = coh_load(&st->free_count);
     const long long cons = used < nf ? used : nf;
-    const long long top = coh_load(&st->pool_top) + (used - cons);
+    long long top = coh_load(&st->pool_top) + (used - cons);
+    top = top < max_blocks ? top : max_blocks;
     coh_store(&st->free_count, nf - cons);
-    coh_store(&st->pool_top, top < max_blocks ? top : max_blocks);
+    coh_store(&st->pool_top, top);
     coh_store(&st->cursor, 0ll);
+    if (rb && seq >= 0) {  // report to the host (vector stores to fine-grained host memory)
+        PoolReport* r = rb + (seq % kReports);
+        __hip_atomic_store(&r->pool_top, top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&r->free_count, nf - cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&r->n_overflow, coh_load(&st->n_overflow), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&r->seq, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // The voxel hash's three-stage launch (u16 + RGB8, obs_weight 1 as HashTable.integrate): as
 // k_fused, with the hash integrate (one wave per brick, in-kernel find-or-insert) and the pool
 // commit done by the integrate workgroup that finishes last (an arrival counter in the batch's
 // list counters; every workgroup's allocations are complete before it arrives).
-template <int = 0>
+template <int DK = 0>
 __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_fused_hash(
         Vol v, Batch bi, Batch bc, Batch bp, Pool pool, Table tab, unsigned long long* stats, Stage sg) {
     __shared__ double s_buf[kRcpTab];
@@ -1115,7 +1145,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_H
         for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedWG / 64;
-        integrate_list<true, 0, 0, true, 8>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
+        integrate_list<true, DK, 0, true, 8>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
                                             sg.gi * wpg, s_stat, s_buf);
         __syncthreads();
         flush_stats(s_stat, stats);
@@ -1126,7 +1156,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_H
         __syncthreads();
         if (s_last && tid == 0) {
             __threadfence();
-            commit_pool(tab.st, tab.max_blocks);
+            commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq);
         }
     } else if (b < sg.gi + sg.gc) {
         cull_superbrick<true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf, s_stat);
@@ -1134,7 +1164,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_H
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;
         float(*sa)[33] = (float(*)[33])s_buf;
-        prep_vec_tile(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
+        prep_vec_tile<DK>(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
     }
 }
 

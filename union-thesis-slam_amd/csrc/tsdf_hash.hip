@@ -9,8 +9,10 @@
 // free list.  A voxel "entry" (count_num_hash_entries, get_hash_entry) is one bit of the
 // block's 512-bit occupancy mask, set by integrate or by an explicit insert.
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "tsdf_host.h"
 
@@ -23,6 +25,17 @@ struct tsdf_hash {
     ListEntry* d_list = nullptr;  // re-run list
     int list_cap = 0;
     bool fused = true;  // three-stage launches (k_fused_hash) when a call allows them
+    // Asynchronous calls (TSDF_ASYNC): every allocating launch reports its pool state into
+    // page-locked host memory (PoolReport, slot seq % kReports); before issuing launch s the host
+    // reads launch s-2's report and grows the pool / table while there is still room for the
+    // launches in flight, so no brick has to be skipped.  A skipped brick cannot be re-run
+    // exactly later (its batch's frames are gone), so it is reported as TSDF_E_CAPACITY.
+    PoolReport* h_rb = nullptr;   // host view of the report slots (hipHostMalloc, mapped)
+    long long seq = 0;            // allocating launches issued so far
+    long long rb_used = -1;       // live blocks in the last report read
+    long long max_delta = 0;      // largest growth of live blocks between two reports
+    long long tomb_est = 0;       // tombstones at the last table scan (only remove() adds them)
+    bool async_pending = false;   // asynchronous launches since the last overflow check
 };
 
 namespace {
@@ -38,7 +51,9 @@ __global__ void k_fill_keys(unsigned long long* k, long long n) {
 }
 
 // After each allocating launch: fold the launch's allocations into the pool state.
-__global__ void k_commit(PoolState* st, long long max_blocks) { commit_pool(st, max_blocks); }
+__global__ void k_commit(PoolState* st, long long max_blocks, PoolReport* rb, long long seq) {
+    commit_pool(st, max_blocks, rb, seq);
+}
 
 // Single-thread linear probe; returns the slot or -1.
 __device__ long long probe_find(const Table& t, unsigned long long key, long long home) {
@@ -261,6 +276,29 @@ __global__ void k_fill_dense(float* t, float* w, float* c, size_t n) {
     }
 }
 
+// Device buffers freed on every exit path unless keep() is called (the error paths of a
+// multi-buffer allocation free what was already allocated).
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() {
+        for (void* q : p)
+            if (q) (void)hipFree(q);
+    }
+    void* add(void* q) {
+        p.push_back(q);
+        return q;
+    }
+    void keep() { p.clear(); }
+};
+
+template <typename T>
+int dev_alloc(DevBufs& bufs, T** out, size_t bytes) {
+    *out = nullptr;
+    TSDF_HIP(hipMalloc((void**)out, bytes));
+    bufs.add(*out);
+    return TSDF_OK;
+}
+
 int read_state(tsdf_hash* h) {
     TSDF_HIP(hipMemcpyAsync(&h->host_st, h->t.st, sizeof(PoolState), hipMemcpyDeviceToHost, h->b.stream));
     TSDF_HIP(hipStreamSynchronize(h->b.stream));
@@ -270,24 +308,27 @@ int read_state(tsdf_hash* h) {
 int grow_pool(tsdf_hash* h, long long new_max) {
     Base& B = h->b;
     Table& t = h->t;
+    // the volume has n_bricks bricks: a pool never needs more blocks than that
+    new_max = std::min<long long>(new_max, B.n_bricks);
+    if (new_max <= t.max_blocks) return TSDF_OK;
     const size_t old_n = (size_t)t.max_blocks, nn = (size_t)new_max;
-    float* nt = nullptr;
-    float* nw = nullptr;
-    float* nc = nullptr;
-    unsigned long long* no = nullptr;
-    int* nf = nullptr;
+    float *nt, *nw, *nc;
+    unsigned long long* no;
+    int* nf;
     TSDF_HIP(hipStreamSynchronize(B.stream));
-    TSDF_HIP(hipMalloc(&nt, nn * kBrickVox * sizeof(float)));
-    TSDF_HIP(hipMalloc(&nw, nn * kBrickVox * sizeof(float)));
-    TSDF_HIP(hipMalloc(&nc, nn * kBrickVox * sizeof(float)));
-    TSDF_HIP(hipMalloc(&no, nn * 8 * sizeof(unsigned long long)));
-    TSDF_HIP(hipMalloc(&nf, nn * sizeof(int)));
+    DevBufs fresh;  // freed again if any allocation or copy fails
+    TSDF_TRY(dev_alloc(fresh, &nt, nn * kBrickVox * sizeof(float)));
+    TSDF_TRY(dev_alloc(fresh, &nw, nn * kBrickVox * sizeof(float)));
+    TSDF_TRY(dev_alloc(fresh, &nc, nn * kBrickVox * sizeof(float)));
+    TSDF_TRY(dev_alloc(fresh, &no, nn * 8 * sizeof(unsigned long long)));
+    TSDF_TRY(dev_alloc(fresh, &nf, nn * sizeof(int)));
     TSDF_HIP(hipMemcpyAsync(nt, B.pool.tsdf, old_n * kBrickVox * sizeof(float), hipMemcpyDeviceToDevice, B.stream));
     TSDF_HIP(hipMemcpyAsync(nw, B.pool.weight, old_n * kBrickVox * sizeof(float), hipMemcpyDeviceToDevice, B.stream));
     TSDF_HIP(hipMemcpyAsync(nc, B.pool.color, old_n * kBrickVox * sizeof(float), hipMemcpyDeviceToDevice, B.stream));
     TSDF_HIP(hipMemcpyAsync(no, t.occ, old_n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, B.stream));
     TSDF_HIP(hipMemcpyAsync(nf, t.free_list, old_n * sizeof(int), hipMemcpyDeviceToDevice, B.stream));
     TSDF_HIP(hipStreamSynchronize(B.stream));
+    fresh.keep();
     (void)hipFree(B.pool.tsdf);
     (void)hipFree(B.pool.weight);
     (void)hipFree(B.pool.color);
@@ -306,13 +347,15 @@ int resize_table(tsdf_hash* h, long long new_cap) {
     Base& B = h->b;
     Table nt = h->t;
     nt.capacity = new_cap;
-    TSDF_HIP(hipMalloc(&nt.keys, sizeof(unsigned long long) * new_cap));
-    TSDF_HIP(hipMalloc(&nt.vals, sizeof(int) * new_cap));
+    DevBufs fresh;
+    TSDF_TRY(dev_alloc(fresh, &nt.keys, sizeof(unsigned long long) * new_cap));
+    TSDF_TRY(dev_alloc(fresh, &nt.vals, sizeof(int) * new_cap));
     hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, nt.keys, (long long)new_cap);
     TSDF_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_rehash, dim3(2048), dim3(256), 0, B.stream, h->t, nt);
     TSDF_HIP(hipGetLastError());
     TSDF_HIP(hipStreamSynchronize(B.stream));
+    fresh.keep();
     (void)hipFree(h->t.keys);
     (void)hipFree(h->t.vals);
     h->t.keys = nt.keys;
@@ -340,10 +383,71 @@ int info_raw(tsdf_hash* h, InfoDev* out) {
 int ensure_room(tsdf_hash* h) {
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
+    h->tomb_est = (long long)inf.tomb;
     TSDF_TRY(read_state(h));
-    if (h->host_st.pool_top + 64 >= h->t.max_blocks && h->host_st.free_count < 64)
+    // the block pool keeps the same headroom as the table: live blocks below 0.75 of it
+    if ((double)(h->host_st.pool_top - h->host_st.free_count + 64) >= 0.75 * (double)h->t.max_blocks)
         TSDF_TRY(grow_pool(h, h->t.max_blocks * 2));
     if ((double)(inf.used + inf.tomb) >= 0.75 * (double)h->t.capacity)
+        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+    return TSDF_OK;
+}
+
+// Bricks skipped by asynchronous launches: their batches' frames are gone, so they cannot be
+// re-run exactly; report them (once) and clear the overflow list so that no later synchronous
+// call replays them against its own frames.
+int take_overflow(tsdf_hash* h) {
+    Base& B = h->b;
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    TSDF_TRY(read_state(h));
+    h->async_pending = false;
+    const long long n = h->host_st.n_overflow;
+    if (n <= 0) return TSDF_OK;
+    TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    h->host_st.n_overflow = 0;
+    return set_error(TSDF_E_CAPACITY,
+                     "asynchronous hash integrate skipped %lld brick updates: the block pool (%lld) or table "
+                     "(%lld slots) filled faster than it could grow; use synchronous calls or a larger "
+                     "max_blocks / capacity",
+                     n, (long long)h->t.max_blocks, (long long)h->t.capacity);
+}
+
+// Report of allocating launch s (written by its committing thread; waits for it).
+int wait_report(tsdf_hash* h, long long s, PoolReport* out) {
+    volatile PoolReport* r = h->h_rb + (s % kReports);
+    for (int spin = 0;; ++spin) {
+        if (__atomic_load_n(&r->seq, __ATOMIC_ACQUIRE) == s + 1) break;
+        if (spin > 64) {
+            const hipError_t q = hipStreamQuery(h->b.stream);
+            if (q == hipSuccess && __atomic_load_n(&r->seq, __ATOMIC_ACQUIRE) != s + 1)
+                return set_error(TSDF_E_HIP, "pool report %lld missing after the stream drained", s);
+            if (q != hipSuccess && q != hipErrorNotReady) TSDF_HIP(q);
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    out->pool_top = r->pool_top;
+    out->free_count = r->free_count;
+    out->n_overflow = r->n_overflow;
+    out->seq = s + 1;
+    return TSDF_OK;
+}
+
+// Asynchronous calls, before issuing allocating launch s: launches s-1 and s may allocate before
+// the next check, so keep room for three times the largest growth seen between two launches.
+int async_room(tsdf_hash* h, long long s) {
+    if (s < 2) return TSDF_OK;
+    PoolReport r;
+    TSDF_TRY(wait_report(h, s - 2, &r));
+    if (r.n_overflow > 0) return take_overflow(h);
+    const long long used = r.pool_top - r.free_count;
+    if (h->rb_used >= 0 && used > h->rb_used) h->max_delta = std::max(h->max_delta, used - h->rb_used);
+    h->rb_used = used;
+    // (a growth estimate of at least 1/12 of the pool keeps the reference's 0.75 load factor)
+    const long long step = std::max<long long>({h->max_delta, h->t.max_blocks / 12, 64});
+    const long long need = used + 3 * step;
+    if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, 2 * need)));
+    while ((double)(used + 3 * std::max<long long>(h->max_delta, 64) + h->tomb_est) >= 0.75 * (double)h->t.capacity)
         TSDF_TRY(resize_table(h, h->t.capacity * 2));
     return TSDF_OK;
 }
@@ -391,7 +495,8 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
             TSDF_TRY(resize_table(h, h->t.capacity * 2));
         launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
         TSDF_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+        hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
+                           (PoolReport*)nullptr, -1ll);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(read_state(h));
     }
@@ -404,7 +509,7 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
 // before launch L+1 is issued; its re-run reads batch L's frames, which no launch has replaced.
 // The cull of batch L+1 already ran, which a resize cannot invalidate: it reads the table only
 // for shard ownership, fixed at create (Table::shard_cap).
-int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, const void* color, int H, int W,
+int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int H, int W,
                    const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     const bool sync = !(flags & TSDF_ASYNC);
@@ -420,7 +525,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, const void* co
             const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
             B.use_set(jp % kSets);
             // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
-            TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, TSDF_DEPTH_U16_MM, color, TSDF_COLOR_RGB8, H, W,
+            TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, dk, color, TSDF_COLOR_RGB8, H, W,
                                      K, Tinv, nullptr, 1.0, flags, f0, n, jp % kSlots));
         }
         const bool has_i = L >= 0, has_c = L + 1 >= 0 && L + 1 < nb, has_p = jp < nb;
@@ -444,16 +549,26 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, const void* co
         if (has_p) sg.count_p = B.count_set[jp % kSets];
         const long long grid = (long long)sg.gi + sg.gc + (has_p ? (long long)sg.ptx * sg.pty * bp.n : 0);
         if (grid >= (1ll << 31)) return set_error(TSDF_E_ARG, "fused grid too large");
+        if (has_i) {
+            if (!sync) TSDF_TRY(async_room(h, h->seq));
+            sg.seq = h->seq++;
+        } else {
+            sg.seq = -1;
+        }
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
-        hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, bc, bp,
-                           B.pool, h->t, B.stats, sg);
+        if (dk == TSDF_DEPTH_U16_MM)
+            hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, bc,
+                               bp, B.pool, h->t, B.stats, sg);
+        else
+            hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, bc,
+                               bp, B.pool, h->t, B.stats, sg);
         TSDF_HIP(hipGetLastError());
         if (!has_i) continue;
         TSDF_TRY(B.prof.end(B.stream, e0));
         B.frames += bi.n;
         if (sync) {
-            TSDF_TRY(hash_after_batch(h, bi, TSDF_DEPTH_U16_MM, TSDF_COLOR_RGB8));
+            TSDF_TRY(hash_after_batch(h, bi, dk, TSDF_COLOR_RGB8));
             TSDF_TRY(B.end_batch(flags, L % kSlots));
             TSDF_TRY(ensure_room(h));
         } else {
@@ -469,14 +584,17 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_HIP(hipSetDevice(B.device));
     const unsigned cull_grid = B.cull_grid();
     const bool sync = !(flags & TSDF_ASYNC);
+    if (sync && h->async_pending) TSDF_TRY(take_overflow(h));  // before any replay of this call
+    if (!sync) h->async_pending = true;
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
-    bool fused = h->fused && dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
+    bool fused = h->fused && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
     if (fused && (flags & TSDF_DEVICE_PTRS))
-        fused = (uintptr_t)depth % 8 == 0 && (uintptr_t)color % 4 == 0 && ((size_t)H * W) % 4 == 0;
+        fused = (uintptr_t)depth % (dk == TSDF_DEPTH_U16_MM ? 8 : 16) == 0 && (uintptr_t)color % 4 == 0 &&
+                ((size_t)H * W) % 4 == 0;
     if (fused) {
-        TSDF_TRY(hash_run_fused(h, n_frames, depth, color, H, W, K, Tinv, flags));
+        TSDF_TRY(hash_run_fused(h, n_frames, depth, dk, color, H, W, K, Tinv, flags));
         TSDF_TRY(guard.finish());
         if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
         return TSDF_OK;
@@ -492,12 +610,14 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         hipLaunchKernelGGL((k_cull<true>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, h->t, B.list,
                            B.count, B.stats);
         TSDF_HIP(hipGetLastError());
+        if (!sync) TSDF_TRY(async_room(h, h->seq));
         hipEvent_t e0;
         TSDF_TRY(B.prof.begin(B.stream, &e0));
         launch_integrate(h, bt, dk, ck, B.list, B.count, 0);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
-        hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+        hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
+                           h->t.rb, h->seq++);
         TSDF_HIP(hipGetLastError());
         B.frames += n;
         if (!sync) {
@@ -511,6 +631,19 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_TRY(guard.finish());
     if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
     return TSDF_OK;
+}
+
+// Run the deferred frames (TSDF_DEFER) as one batch from their bounce slot, synchronously: a
+// full table or pool is then grown and the skipped bricks re-run exactly (hash_after_batch).
+int hash_flush(tsdf_hash* h) {
+    Base& B = h->b;
+    if (B.dfr.n == 0) return TSDF_OK;
+    const Base::Deferred d = B.dfr;
+    B.dfr.n = 0;
+    B.prestaged = d.slot;
+    const int r = hash_run(h, d.n, B.hst_depth[d.slot], d.dk, B.hst_color[d.slot], d.ck, d.H, d.W, d.K, d.T, 0);
+    B.prestaged = -1;
+    return r;
 }
 
 int upload(tsdf_hash* h, const void* src, size_t bytes, void** dst) {
@@ -535,18 +668,6 @@ std::vector<unsigned long long> unique_blocks(const Vol& v, const int64_t* ijk, 
     return keys;
 }
 
-struct DevBufs {
-    std::vector<void*> p;
-    ~DevBufs() {
-        for (void* q : p)
-            if (q) (void)hipFree(q);
-    }
-    void* add(void* q) {
-        p.push_back(q);
-        return q;
-    }
-};
-
 }  // namespace
 
 extern "C" {
@@ -566,7 +687,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         h->b.vol.shard = shard;
         h->b.vol.n_shards = n_shards;
         if (max_blocks <= 0) max_blocks = std::min<long long>(h->b.n_bricks, 1 << 16);
-        max_blocks = std::max<long long>(max_blocks, 64);
+        max_blocks = std::max<long long>(std::min<long long>(max_blocks, h->b.n_bricks), 64);
         t.capacity = capacity;
         t.shard_cap = capacity;
         t.max_blocks = max_blocks;
@@ -581,6 +702,11 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         if (e == hipSuccess) e = hipMalloc(&h->b.pool.tsdf, sizeof(float) * kBrickVox * max_blocks);
         if (e == hipSuccess) e = hipMalloc(&h->b.pool.weight, sizeof(float) * kBrickVox * max_blocks);
         if (e == hipSuccess) e = hipMalloc(&h->b.pool.color, sizeof(float) * kBrickVox * max_blocks);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_rb, sizeof(PoolReport) * kReports, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            std::memset(h->h_rb, 0, sizeof(PoolReport) * kReports);
+            e = hipHostGetDevicePointer((void**)&t.rb, h->h_rb, 0);
+        }
         if (e != hipSuccess)
             r = set_error(e == hipErrorOutOfMemory ? TSDF_E_OOM : TSDF_E_HIP, "hash allocation: %s",
                           hipGetErrorString(e));
@@ -605,6 +731,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
                   h->b.pool.tsdf, h->b.pool.weight, h->b.pool.color, h->d_list};
     for (void* p : ps)
         if (p) (void)hipFree(p);
+    if (h->h_rb) (void)hipHostFree(h->h_rb);
     delete h;
     return TSDF_OK;
 }
@@ -612,6 +739,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
 int tsdf_hash_reset(tsdf_hash_t* h) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     Base& B = h->b;
+    B.dfr.n = 0;  // deferred frames are dropped with the state
     TSDF_HIP(hipSetDevice(B.device));
     hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, h->t.keys, (long long)h->t.capacity);
     TSDF_HIP(hipGetLastError());
@@ -620,6 +748,10 @@ int tsdf_hash_reset(tsdf_hash_t* h) {
     TSDF_HIP(hipStreamSynchronize(B.stream));
     B.frames = 0;
     std::memset(&h->host_st, 0, sizeof(h->host_st));
+    h->rb_used = -1;
+    h->max_delta = 0;
+    h->tomb_est = 0;
+    h->async_pending = false;
     return TSDF_OK;
 }
 
@@ -628,6 +760,17 @@ int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const
                         const double world_to_cam[16], int flags) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    TSDF_HIP(hipSetDevice(h->b.device));
+    Base& B = h->b;
+    if (flags & TSDF_DEFER) {
+        if (flags & TSDF_DEVICE_PTRS) return set_error(TSDF_E_ARG, "TSDF_DEFER takes host frames only");
+        if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(hash_flush(h));
+        // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1
+        TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0));
+        if (B.dfr.n == kMaxBatch) TSDF_TRY(hash_flush(h));
+        return TSDF_OK;
+    }
+    TSDF_TRY(hash_flush(h));
     return hash_run(h, 1, depth, depth_kind, color, color_kind, height, width, K, world_to_cam, flags);
 }
 
@@ -638,6 +781,8 @@ int tsdf_hash_integrate_batch(tsdf_hash_t* h, int n_frames, const void* depth, i
     if (n_frames < 0) return set_error(TSDF_E_ARG, "n_frames < 0");
     if (n_frames == 0) return TSDF_OK;
     TSDF_TRY(check_frame_args(depth, depth_kind, color, color_kind, height, width, K, world_to_cam));
+    TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(hash_flush(h));
     return hash_run(h, n_frames, depth, depth_kind, color, color_kind, height, width, K,
                     world_to_cam, flags);
 }
@@ -648,6 +793,7 @@ int tsdf_hash_lookup(tsdf_hash_t* h, const int64_t* ijk, int64_t n, float* tsdf_
     if (n == 0) return TSDF_OK;
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
     DevBufs bufs;
     void *dijk, *dt = nullptr, *dw = nullptr, *dc = nullptr, *df = nullptr;
     TSDF_TRY(upload(h, ijk, sizeof(int64_t) * 3 * n, &dijk));
@@ -682,6 +828,7 @@ int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float*
                              (long long)x, (long long)y, (long long)z, v.dims[0], v.dims[1], v.dims[2]);
     }
     TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
     std::vector<unsigned long long> keys = unique_blocks(v, ijk, n);
     const long long nk = (long long)keys.size();
     // room first (the reference resizes before inserting, hash_fusion.py:208-209)
@@ -705,7 +852,8 @@ int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float*
     hipLaunchKernelGGL(k_insert_blocks, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, B.stream, h->t,
                        B.pool, (const unsigned long long*)dkeys, (long long)nk, (int*)dblk, (long long*)dslot);
     TSDF_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks);
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
+                       (PoolReport*)nullptr, -1ll);
     TSDF_HIP(hipGetLastError());
     TSDF_TRY(upload(h, ijk, sizeof(int64_t) * 3 * n, &dijk));
     bufs.add(dijk);
@@ -743,6 +891,7 @@ int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* rem
     if (n == 0) return TSDF_OK;
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
     std::vector<unsigned long long> keys = unique_blocks(B.vol, ijk, n);
     DevBufs bufs;
     void *dijk, *dkeys, *drem = nullptr;
@@ -770,6 +919,7 @@ int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* rem
 int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(hash_flush(h));
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
     if (new_capacity <= (int64_t)inf.used) return set_error(TSDF_E_ARG, "new capacity too small");
@@ -779,6 +929,7 @@ int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity) {
 int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out) {
     if (!h || !out) return set_error(TSDF_E_ARG, "null pointer");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(hash_flush(h));
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
     TSDF_TRY(read_state(h));
@@ -797,6 +948,7 @@ int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf_, float* weight_, float* col
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
     const size_t n = (size_t)B.vol.dims[0] * B.vol.dims[1] * B.vol.dims[2];
     DevBufs bufs;
     void *dt = nullptr, *dw = nullptr, *dc = nullptr;
@@ -818,19 +970,23 @@ int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf_, float* weight_, float* col
 int tsdf_hash_sync(tsdf_hash_t* h) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(hash_flush(h));
     TSDF_HIP(hipStreamSynchronize(h->b.stream));
+    if (h->async_pending) TSDF_TRY(take_overflow(h));
     return TSDF_OK;
 }
 
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(hash_flush(h));
     return h->b.read_stats(out, reset);
 }
 
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
+    TSDF_TRY(hash_flush(h));
     return h->b.set_profiling(on);
 }
 

@@ -100,6 +100,23 @@ struct Base {
     void* hst_depth[kSlots] = {};      // page-locked bounce slots (hipHostMalloc)
     void* hst_color[kSlots] = {};
 
+    // Deferred single frames (TSDF_DEFER, the reference's one-integrate()-per-frame call
+    // pattern): each call copies its frame straight into bounce slot `slot` and returns; every
+    // kMaxBatch frames (or at any other call on the handle) the collected frames run as one
+    // asynchronous batch -- temporal batching for per-frame callers, same results.
+    struct Deferred {
+        int n = 0, H = 0, W = 0, dk = 0, ck = 0, slot = -1;
+        double K[9];
+        double T[16 * kMaxBatch];
+        double ow[kMaxBatch];
+    } dfr;
+    int defer_next = 0;   // bounce slot of the next deferred batch
+    int prestaged = -1;   // >= 0: the call's (single) batch already sits in this bounce slot
+    bool defer_same(int dk, int ck, int H, int W, const double* K) const;
+    int defer_push(const void* depth, int dk, const void* color, int ck, int H, int W,
+                   const double* K, const double* T, double ow);
+    int stage_alloc(size_t dbytes, size_t cbytes);  // bounce + device staging slots (per frame)
+
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
     int use_sets(int n);  // allocate n buffer sets (1 or kSets)

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("TSDF_HIP_LIB") or os.path.join(_HERE, "lib", "libtsdf
 
 DEPTH_U16_MM, DEPTH_F64_M = 0, 1
 COLOR_RGB8, COLOR_F32 = 0, 1
-DEVICE_PTRS, ASYNC, DEPTH_INVALID_65535 = 1, 2, 4
+DEVICE_PTRS, ASYNC, DEPTH_INVALID_65535, DEFER = 1, 2, 4, 8
 
 E_ARG, E_HIP, E_NODEV, E_CAPACITY, E_OOM = -1, -2, -3, -4, -5
 
@@ -136,14 +136,16 @@ def call(name: str, *args) -> None:
 
 
 def ptr(a) -> ctypes.c_void_p | None:
-    """Address of a C-contiguous ndarray (or None)."""
+    """Address of a C-contiguous ndarray (or None).  The returned pointer object holds a
+    reference to the array (ndarray.ctypes.data_as), so a temporary passed straight into a call,
+    e.g. ptr(f64(K, 9)), stays alive until the call returns."""
     if a is None:
         return None
     if isinstance(a, int):
         return ctypes.c_void_p(a)
     if not a.flags["C_CONTIGUOUS"]:
         raise ValueError("array must be C-contiguous")
-    return ctypes.c_void_p(a.ctypes.data)
+    return a.ctypes.data_as(ctypes.c_void_p)
 
 
 def device_count() -> int:

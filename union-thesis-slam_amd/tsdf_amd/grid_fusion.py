@@ -8,8 +8,11 @@ module only does the reference's host-side duties:
   * volume geometry, including the in-place rewrite of vol_bnds[:,1] (grid_fusion.py:31-44);
   * inv(cam_pose) with NumPy/LAPACK, as the reference does on the host (grid_fusion.py:265);
   * the colour fold for non-uint8 input (grid_fusion.py:228-232);
-  * depth: uint16 millimetres are sent when they reproduce the float64 metres exactly
-    (mm / 1000.0 == depth bit for bit, the demos' ingest), else the float64 metres themselves.
+  * depth: float64 metres are sent as they are (uint16 millimetres when the caller has them);
+  * per-frame integrate() calls are deferred into pinned staging batches of 8 frames (TSDF_DEFER)
+    that run as one temporally batched launch; every other call (get_volume, get_state, stats,
+    sync, meshing, batch integrate) runs the pending frames first, so results and their order
+    are those of one-by-one integration.  `defer=False` makes each call synchronous.
 """
 from __future__ import annotations
 
@@ -34,19 +37,13 @@ def volume_geometry(vol_bnds, voxel_size):
 
 
 def encode_depth(depth_im):
-    """(kind, contiguous array) for the C-ABI.  uint16 input is taken as millimetres."""
+    """(kind, contiguous array) for the C-ABI.  uint16 input is taken as millimetres; anything
+    else goes as float64 metres, the reference's own depth_im, read by the kernels as is (no host
+    pass over the image)."""
     d = np.asarray(depth_im)
     if d.dtype == np.uint16:
         return _ffi.DEPTH_U16_MM, np.ascontiguousarray(d)
-    d = np.ascontiguousarray(d, dtype=np.float64)
-    with np.errstate(invalid="ignore", over="ignore"):
-        mm = np.rint(d * 1000.0)
-        ok = bool(np.all((mm >= 0) & (mm <= 65535)))
-        if ok:
-            mm16 = mm.astype(np.uint16)
-            if np.array_equal((mm16.astype(np.float64) / 1000.0).view(np.uint64), d.view(np.uint64)):
-                return _ffi.DEPTH_U16_MM, mm16
-    return _ffi.DEPTH_F64_M, d
+    return _ffi.DEPTH_F64_M, np.ascontiguousarray(d, dtype=np.float64)
 
 
 def encode_color(color_im):
@@ -91,10 +88,14 @@ class TSDFVolume:
       device: HIP device index.  slab: (x_begin, x_end) voxel range of this shard along x.
       shard: (rank, world) cyclic brick-column shard (sharding.columns) -- the bench's layout.
       `x_index` holds the global x of every local x row either way.
+      defer: integrate() collects frames into batches of 8 (TSDF_DEFER); False: one synchronous
+      call per frame.
     """
 
-    def __init__(self, vol_bnds, voxel_size, use_gpu=True, *, device=0, slab=None, shard=None):
+    def __init__(self, vol_bnds, voxel_size, use_gpu=True, *, device=0, slab=None, shard=None,
+                 defer=True):
         print("Initializing voxel grids ... ")
+        self.defer = bool(defer)
         self._vol_bnds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
             vol_bnds, voxel_size)
         self._trunc_margin = 5 * self._voxel_size
@@ -142,7 +143,7 @@ class TSDFVolume:
         K = _ffi.f64(cam_intr, 9)
         Tinv = _ffi.f64(np.linalg.inv(np.asarray(cam_pose, dtype=np.float64)), 16)
         _ffi.call("tsdf_dense_integrate", self._h, _ffi.ptr(d), dk, _ffi.ptr(c), ck, im_h, im_w,
-                  _ffi.ptr(K), _ffi.ptr(Tinv), float(obs_weight), 0)
+                  _ffi.ptr(K), _ffi.ptr(Tinv), float(obs_weight), _ffi.DEFER if self.defer else 0)
 
     def get_volume(self):
         """(tsdf, colour) float32 C-order (X,Y,Z) host arrays (grid_fusion.py:316-320)."""

@@ -42,12 +42,14 @@ class HashTable:
     Args as hash_fusion.py:34: vol_bounds (3,2) metres (column 1 rewritten in place),
     voxel_size, map_size (table slots), load_factor / use_gpu (accepted, ignored like the
     reference).  Keyword-only: int_bits (64|32), max_blocks (initial pool size; grows),
-    device, shard / n_shards (bucket-range ownership for multi-GPU).
+    device, shard / n_shards (bucket-range ownership for multi-GPU), defer
+    (integrate() collects frames into batches of 8, as TSDFVolume).
     """
 
     def __init__(self, vol_bounds, voxel_size, map_size=1000000, load_factor=0.75, use_gpu=False,
-                 *, int_bits=64, max_blocks=None, device=0, shard=0, n_shards=1):
+                 *, int_bits=64, max_blocks=None, device=0, shard=0, n_shards=1, defer=True):
         self._load_factor = 0.75
+        self.defer = bool(defer)
         self._vol_bounds, self._vol_dim, self._vol_origin, self._voxel_size = volume_geometry(
             vol_bounds, voxel_size)
         self._trunc_margin = 5 * self._voxel_size
@@ -87,7 +89,7 @@ class HashTable:
         K = _ffi.f64(cam_intr, 9)
         Tinv = _ffi.f64(np.linalg.inv(np.asarray(cam_pose, dtype=np.float64)), 16)
         _ffi.call("tsdf_hash_integrate", self._h, _ffi.ptr(d), dk, _ffi.ptr(c), ck, im_h, im_w,
-                  _ffi.ptr(K), _ffi.ptr(Tinv), 0)
+                  _ffi.ptr(K), _ffi.ptr(Tinv), _ffi.DEFER if self.defer else 0)
 
     def integrate_batch(self, depth, color, cam_intr, world_to_cam, *, depth_kind=None,
                         color_kind=None, hw=None, device_ptrs=False, sync=True, invalid_65535=False):

@@ -22,6 +22,10 @@ FX = FY = 585.0
 CX, CY = 320.0, 240.0
 W, H = 640, 480
 ROOM = 10.24  # metres; 512 voxels at 2 cm
+# The bench's camera ring (trajectory radius_frac and make_spheres ring_frac): mean V_f = 11.7 %
+# of the 512^3 volume over the 1000-frame loop (min 7.9 %, max 16.8 %; SURVEY §8(d) asks for
+# 10-20 %).  The tests keep the default 0.34 ring (8.9 %), which their fixtures were made with.
+BENCH_RING = 0.42
 
 
 def intrinsics() -> np.ndarray:
@@ -29,16 +33,17 @@ def intrinsics() -> np.ndarray:
     return np.array([[FX, 0.0, CX], [0.0, FY, CY], [0.0, 0.0, 1.0]], dtype=np.float64)
 
 
-def make_spheres(seed: int = 0, n: int = 10, room: float = ROOM) -> np.ndarray:
-    """(n, 4) float64 [cx, cy, cz, r]: seeded spheres kept off the camera ring."""
+def make_spheres(seed: int = 0, n: int = 10, room: float = ROOM, ring_frac: float = 0.34) -> np.ndarray:
+    """(n, 4) float64 [cx, cy, cz, r]: seeded spheres kept off the camera ring (radius
+    ring_frac * room around the centre, see trajectory's radius_frac)."""
     rng = np.random.default_rng(seed)
     out = []
     c = room / 2
     while len(out) < n:
         r = rng.uniform(0.35, 1.1)
         p = rng.uniform(1.2 + r, room - 1.2 - r, size=3)
-        # keep the camera ring (radius ~0.34*room around the centre, mid height) free
-        ring_d = abs(math.hypot(p[0] - c, p[1] - c) - 0.34 * room)
+        # keep the camera ring (radius ~ring_frac*room around the centre, mid height) free
+        ring_d = abs(math.hypot(p[0] - c, p[1] - c) - ring_frac * room)
         if ring_d < r + 0.6 and abs(p[2] - c) < r + 1.2:
             continue
         out.append([p[0], p[1], p[2], r])
