@@ -135,9 +135,30 @@ int tsdf_dense_sync(tsdf_dense_t* h);
  * round(vertex) (grid_fusion.py:336-346), faces n_tris x 3 int32 vertex ids.  One vertex per
  * grid edge whose end values straddle 0 (one below 0, one not), at the linear interpolation;
  * vertices ordered by (voxel, axis) in C-order and shared by the cells around the edge.  Any
- * output pointer may be NULL.  A shard is meshed on its own (no cells across shard borders). */
+ * output pointer may be NULL.  Vertex world x comes from the GLOBAL voxel index, so a slab
+ * shard meshed alone gives the mesh of its own sub-volume in world coordinates; a cyclic column
+ * shard needs its neighbours' border rows (tsdf_dense_extract_mesh_halo), else TSDF_E_ARG. */
 int tsdf_dense_extract_mesh(tsdf_dense_t* h, int64_t* n_verts, int64_t* n_tris);
 int tsdf_dense_get_mesh(tsdf_dense_t* h, float* verts, float* normals, uint8_t* colors, int32_t* faces);
+/* Sharded marching cubes.  mesh_halo_rows: the global x rows (sorted) of the
+ * unsharded volume (x extent global_x) that this shard's cells and gradients read but do not
+ * own; with rows == NULL only *n_rows is set, else rows must hold *n_rows >= that many.
+ * extract_mesh_halo: marching cubes over the cells anchored at the shard's own rows, given those
+ * rows (halo_gx[n_halo] global x, halo_tsdf / halo_color n_halo x Y x Z C-order float32; host, or
+ * device with TSDF_DEVICE_PTRS).  The shard's mesh holds its own cells' triangles and every
+ * vertex they use, including copies of the next shard's border vertices; get_mesh_keys gives
+ * each vertex's global identity ((x*Y + y)*Z + z)*3 + axis, the order of the unsharded mesh,
+ * so the union of the shards' meshes, vertices merged by key, is the unsharded mesh. */
+int tsdf_dense_mesh_halo_rows(tsdf_dense_t* h, int64_t global_x, int64_t* rows, int64_t* n_rows);
+int tsdf_dense_extract_mesh_halo(tsdf_dense_t* h, int64_t global_x, const int64_t* halo_gx, int64_t n_halo,
+                                 const float* halo_tsdf, const float* halo_color, int flags, int64_t* n_verts,
+                                 int64_t* n_tris);
+int tsdf_dense_get_mesh_keys(tsdf_dense_t* h, int64_t* keys);
+/* Local x rows (rows[n_rows], local indices) of the shard in C-order (n_rows, Y, Z) float32 -- the
+ * halo rows another shard needs and the rows of a device-side gather (get_volume of a sharded
+ * volume).  Host pointers, or device pointers with TSDF_DEVICE_PTRS; NULL skips a field. */
+int tsdf_dense_get_rows(tsdf_dense_t* h, const int64_t* rows, int64_t n_rows, float* tsdf, float* weight,
+                        float* color, int flags);
 /* The marching-cubes case table in use: tri[256][16] cube-edge ids (-1 padded; edge e joins the
  * corners differing in bit e / 4 of the corner index, its lower corner's other two bits being
  * e % 4 in increasing bit order), ntri[256] triangles per case.  Host-only; no device needed. */
@@ -182,6 +203,17 @@ int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* rem
 /* double_table_size (hash_fusion.py:414-437): rehash every live key into 2x the slots. */
 int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity);
 int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out);
+/* Sparse block transfer for merging bucket-range shards: only live blocks move.
+ * export: with bxyz == NULL, *n_blocks = live blocks; else fills up to *n_blocks (must be >= the
+ *   live count) blocks: bxyz n x 3 int32 block coordinates, tsdf/weight/color n x 512 float32 in
+ *   brick-local order (x*8 + y)*8 + z, occ n x 8 uint64 voxel-entry words (word z, bit x*8+y);
+ *   any field pointer may be NULL.  Host pointers, or device pointers with TSDF_DEVICE_PTRS.
+ * import: find-or-insert each block (distinct, inside the volume) and overwrite its contents and
+ *   entry words (NULL occ: every voxel has an entry).  The table / pool grow as needed. */
+int tsdf_hash_export_blocks(tsdf_hash_t* h, int32_t* bxyz, float* tsdf, float* weight, float* color,
+                            uint64_t* occ, int64_t* n_blocks, int flags);
+int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_blocks, const float* tsdf,
+                            const float* weight, const float* color, const uint64_t* occ, int flags);
 /* get_volume (hash_fusion.py:442-463): densify into C-order (X,Y,Z) host arrays; voxels
  * without an entry get tsdf 1, weight 0, colour 0.  Any pointer may be NULL. */
 int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf, float* weight, float* color);

@@ -75,6 +75,54 @@ def _hash_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+class _FakeShard:
+    """Host stand-in for a sharded TSDFVolume (the attributes and calls tsdf_amd.sharding uses),
+    backed by an oracle volume's arrays: lets the exchange / gather logic run under gloo on the
+    CPU.  mesh_halo_rows restates csrc/tsdf_mesh.hip mesh_halo_rows."""
+
+    def __init__(self, full, x_index):
+        self.x_index = np.asarray(x_index, np.int64)
+        self._vol_dim = np.array(full[0].shape, np.int64)
+        self._local_dim = np.array([len(self.x_index)] + list(full[0].shape[1:]), np.int64)
+        self._rows = [a[self.x_index] for a in full]
+
+    def mesh_halo_rows(self, global_x=None):
+        X = int(global_x or self._vol_dim[0])
+        local = np.zeros(X, bool)
+        local[self.x_index] = True
+        need = set()
+        for g in self.x_index:
+            need |= {g - 1, g + 1} | ({g + 2} if g + 1 < X and not local[g + 1] else set())
+        return np.array(sorted(g for g in need if 0 <= g < X and not local[g]), np.int64)
+
+    def get_rows(self, local_rows, weight=True, out=None):
+        lr = np.asarray(local_rows, np.int64)
+        t, w, c = (a[lr] for a in self._rows)
+        return t, (w if weight else None), c
+
+
+def _halo_worker(rank, world, port, out_dir):
+    import oracle as O
+    from tsdf_amd import sharding
+    dist = _init(rank, world, port)
+    full = O.OracleTSDFVolume(np.array(C1), 0.04)
+    _, depth, rgb, pose = load_lounge(0)
+    full.integrate(rgb, depth, lounge_intrinsics(), pose)
+    arrs = (full._tsdf_vol_cpu, full._weight_vol_cpu, full._color_vol_cpu)
+    X = arrs[0].shape[0]
+    sh = _FakeShard(arrs, sharding.columns(rank, world, X))
+    gx, ht, hc = sharding.exchange_halo(sh)
+    ok = bool(np.array_equal(gx, sh.mesh_halo_rows()) and np.array_equal(ht, arrs[0][gx])
+              and np.array_equal(hc, arrs[2][gx]))
+    oks = [None] * world
+    dist.all_gather_object(oks, ok)
+    state = sharding.gather_volume(sh)
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "halo.npz"), ok=np.array(oks), t=state[0], w=state[1], c=state[2],
+                 n_halo=len(gx))
+    dist.destroy_process_group()
+
+
 def _cyclic_worker(rank, world, port, out_dir):
     _dense_worker(rank, world, port, out_dir, cyclic=True)
 
@@ -146,3 +194,32 @@ def test_hash_bucket_ranges_two_ranks_gloo(tmp_path):
     assert np.array_equal(g["c"], hv.color.astype(np.float32))
     assert np.array_equal(g["t"], hv.sdf.astype(np.float32))
     assert 0 < int(g["owned"]) < hv.weight.size
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange_and_device_gather_logic_gloo(tmp_path, world):
+    """sharding.exchange_halo (every rank's border rows for sharded marching cubes, traded point
+    to point) and sharding.gather_volume on world_size 2 and 3 over gloo: each rank receives
+    exactly the rows mesh_halo_rows asks for, with the owners' values, and rank 0 reassembles the
+    whole volume."""
+    import oracle as O
+    mp.start_processes(_halo_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    g = np.load(os.path.join(tmp_path, "halo.npz"))
+    assert g["ok"].all() and int(g["n_halo"]) > 0
+    full = O.OracleTSDFVolume(np.array(C1), 0.04)
+    _, depth, rgb, pose = load_lounge(0)
+    full.integrate(rgb, depth, lounge_intrinsics(), pose)
+    assert np.array_equal(g["t"], full._tsdf_vol_cpu) and np.array_equal(g["w"], full._weight_vol_cpu)
+    assert np.array_equal(g["c"], full._color_vol_cpu)
+
+
+def test_merge_meshes_unites_by_key():
+    """merge_meshes: duplicated border vertices collapse to one, ordered by key; faces follow."""
+    from tsdf_amd import sharding
+    v = np.arange(15, dtype=np.float32).reshape(5, 3)
+    a = (v[[0, 1, 2]], np.array([[0, 1, 2]], np.int32), v[[0, 1, 2]], np.zeros((3, 3), np.uint8), np.array([10, 20, 30]))
+    b = (v[[2, 3, 4]], np.array([[0, 2, 1]], np.int32), v[[2, 3, 4]], np.ones((3, 3), np.uint8), np.array([30, 5, 40]))
+    mv, mf, mn, mc = sharding.merge_meshes([a, b])
+    assert np.array_equal(mv, v[[3, 0, 1, 2, 4]])  # keys 5, 10, 20, 30, 40
+    assert np.array_equal(mf, np.array([[1, 2, 3], [3, 4, 0]]))

@@ -1,0 +1,166 @@
+"""Long runs and the per-rank workloads of BASELINE's 8-GPU configs, on one GPU:
+
+  * config[3] per rank: cyclic column shard 3 of 8 of the 512^3 @ 2 cm volume over 1000 frames
+    of the bench trajectory, bit-exact against the oracle on rows of the shard;
+  * the fast-path boundary: weights around the 4087 limit of the LDS reciprocal table
+    (small_int, csrc/tsdf_device.h) and non-canonical colours, preloaded with set_state;
+  * config[4] per rank: bucket-range hash shard 5 of 8 over a 1024^3 @ 1 cm extent with 2^22
+    buckets, against dense slabs (and the oracle) on rows restricted to the shard's blocks;
+  * the hash's f32 state against the reference's float64 Voxel (voxel.py:19-49) over 500 frames,
+    within north_star's 1e-4.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+ROOM = 10.24
+
+
+def _same(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
+
+
+def _frames_on_device(n, start=0, ring=None):
+    """n bench-trajectory frames rendered straight into HBM (u16 bits as int16, RGB8)."""
+    import torch
+    from tsdf_amd import scene
+    ring = scene.BENCH_RING if ring is None else ring
+    poses = scene.trajectory(n, seed=0, start=start, radius_frac=ring)
+    spheres = scene.make_spheres(0, ring_frac=ring)
+    dev = torch.device("cuda", 0)
+    depth = torch.empty((n, 480, 640), dtype=torch.int16, device=dev)
+    rgb = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
+    for s in range(0, n, 50):
+        d, c = scene.render(poses[s:s + 50], spheres, seed=0, start=start + s, device=dev, depth_dtype=torch.int16)
+        depth[s:s + len(d)] = d
+        rgb[s:s + len(c)] = c
+    torch.cuda.synchronize()
+    return depth, rgb, poses
+
+
+def test_config3_rank_shard_1000_frames_matches_oracle_rows():
+    """One rank of config[3]: the cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 1000
+    frames (125 batches through the pipelined launches); rows at both ends of one of its columns
+    and inside two others equal the oracle bit for bit at the end (weights reach the hundreds)."""
+    from tsdf_amd import grid_fusion, scene, sharding
+    n = 1000
+    depth, rgb, poses = _frames_on_device(n)
+    K = scene.intrinsics()
+    Tinv = np.linalg.inv(poses)
+    bnds = np.array([[0.0, ROOM]] * 3)
+    vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(3, 8))
+    vol.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=False)
+    vol.sync()
+    xi = sharding.columns(3, 8, 512)
+    rows = np.array([24, 31, 219, 412], np.int64)  # columns 3, 27, 51 (all c % 8 == 3)
+    assert np.isin(rows, xi).all()
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.02, x_index=rows)
+    dh = depth.cpu().numpy().view(np.uint16)
+    ch = rgb.cpu().numpy()
+    n_upd = 0
+    for f in range(n):
+        n_upd += orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    assert n_upd > 10_000_000
+    lr = np.searchsorted(xi, rows)
+    t, w, c = vol.get_rows(lr)
+    assert _same(t, orc._tsdf_vol_cpu) and _same(w, orc._weight_vol_cpu) and _same(c, orc._color_vol_cpu)
+    assert w.max() >= 500 and vol.stats()["list_errors"] == 0
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched):
+    """Preloaded weights 4078..4100 (the LDS table of RN(1/n) covers integer weights below 4087:
+    small_int switches the quotients to IEEE division mid-run) and colours that are not the
+    canonical B*65536+G*256+R integers (non-integral, negative, >= 2^24), next to canonical ones:
+    every path of the update equals the oracle bit for bit."""
+    from tsdf_amd import grid_fusion, scene
+    n = 12
+    depth, rgb, poses = _frames_on_device(n, start=120, ring=0.34)
+    dh, ch = depth.cpu().numpy().view(np.uint16), rgb.cpu().numpy()
+    K = scene.intrinsics()
+    bnds = np.array([[0.0, ROOM]] * 3)
+    vol = grid_fusion.TSDFVolume(bnds.copy(), 0.08)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
+    shape = tuple(int(x) for x in vol._vol_dim)
+    rng = np.random.default_rng(11)
+    w0 = rng.integers(4078, 4101, size=shape).astype(np.float32)
+    w0[rng.random(shape) < 0.3] = 0.0
+    t0 = rng.uniform(-1, 1, size=shape).astype(np.float32)
+    canon = (rng.integers(0, 256, size=shape) * 65536 + rng.integers(0, 256, size=shape) * 256
+             + rng.integers(0, 256, size=shape)).astype(np.float32)
+    odd = rng.choice(np.array([0.5, -3.0, 16777216.0 + 512.0, 123456.75], np.float32), size=shape)
+    c0 = np.where(rng.random(shape) < 0.25, odd, canon).astype(np.float32)
+    vol.set_state(t0, w0, c0)
+    orc._tsdf_vol_cpu[:], orc._weight_vol_cpu[:], orc._color_vol_cpu[:] = t0, w0, c0
+    for f in range(n):
+        orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    if batched:
+        vol.integrate_batch(dh, ch, K, np.linalg.inv(poses))
+    else:
+        for f in range(n):
+            vol.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    T, W, C = vol.get_state()
+    assert (W > 4087).any() and (W[W > 0] < 4087).any()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+
+
+def test_config4_rank_hash_shard_1024_extent():
+    """One rank of config[4]: bucket-range shard 5 of 8 over a 1024^3 @ 1 cm extent (2^21 bricks,
+    21-bit key fields up to 127), 2^22 buckets, 40 frames.  On three x rows: a voxel is found iff
+    its block's home bucket is in the shard's range and the dense grid updated it, with the dense
+    grid's exact values; the dense rows equal the oracle."""
+    from tsdf_amd import grid_fusion, hash_fusion, scene, sharding
+    n = 40
+    depth, rgb, poses = _frames_on_device(n, start=300)
+    K = scene.intrinsics()
+    Tinv = np.linalg.inv(poses)
+    bnds = np.array([[0.0, ROOM]] * 3)
+    ht = hash_fusion.HashTable(bnds.copy(), 0.01, 1 << 22, shard=5, n_shards=8, max_blocks=1 << 16)
+    assert tuple(int(x) for x in ht._vol_dim) == (1024, 1024, 1024)
+    ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True)
+    rows = [100, 517, 1023]
+    dh, ch = depth.cpu().numpy().view(np.uint16), rgb.cpu().numpy()
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.01, x_index=np.array(rows))
+    for f in range(n):
+        orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    yy, zz = np.meshgrid(np.arange(1024), np.arange(1024), indexing="ij")
+    for i, x in enumerate(rows):
+        sl = grid_fusion.TSDFVolume(bnds.copy(), 0.01, slab=(x, x + 1))
+        sl.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True)
+        T, W, C = (a[0] for a in sl.get_state())
+        assert _same(T, orc._tsdf_vol_cpu[i]) and _same(W, orc._weight_vol_cpu[i]) and _same(C, orc._color_vol_cpu[i])
+        own = sharding.hash_owner(x // 8, yy // 8, zz // 8, 1 << 22, 8) == 5
+        ijk = np.stack([np.full(yy.size, x), yy.reshape(-1), zz.reshape(-1)], 1)
+        found, t, w, c = ht.lookup(ijk)
+        found = found.reshape(1024, 1024)
+        assert np.array_equal(found, own & (W > 0))
+        assert 0 < found.sum() < (W > 0).sum()
+        m = found.reshape(-1)
+        assert _same(t[m], T.reshape(-1)[m]) and _same(w[m], W.reshape(-1)[m]) and _same(c[m], C.reshape(-1)[m])
+    info = ht.info()
+    assert info["used"] > 10_000 and ht.stats()["bricks_skipped"] == 0
+
+
+def test_hash_f32_state_within_1e4_of_reference_f64_voxels_over_500_frames():
+    """HashTable.integrate keeps the reference's Voxel in float64 (voxel.py:19-49); the GPU hash
+    keeps f32 like the grid.  Over 500 frames the voxel set, weights and colours stay equal and
+    tsdf within north_star's 1e-4."""
+    from tsdf_amd import hash_fusion, scene
+    n = 500
+    depth, rgb, poses = _frames_on_device(n, start=0, ring=0.34)
+    K = scene.intrinsics()
+    bnds = np.array([[0.0, ROOM]] * 3)
+    ht = hash_fusion.HashTable(bnds.copy(), 0.08, 1 << 16)
+    ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, np.linalg.inv(poses), hw=(480, 640), device_ptrs=True)
+    hv = O.OracleHashVolume(bnds.copy(), 0.08)
+    dh, ch = depth.cpu().numpy().view(np.uint16), rgb.cpu().numpy()
+    for f in range(n):
+        hv.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    T, W, C = ht.get_state()
+    assert np.array_equal(W > 0, hv.weight > 0)
+    assert np.array_equal(W.astype(np.float64), hv.weight) and np.array_equal(C.astype(np.float64), hv.color)
+    drift = np.abs(T.astype(np.float64) - hv.sdf).max()
+    assert hv.weight.max() >= 400
+    assert drift <= 1e-4, drift

@@ -1,6 +1,7 @@
 // tsdf_dense.hip -- dense TSDF grid: the MI355X replacement of TSDFVolume
 // (grid_fusion.py:19-320).  HBM layout: three f32 SoA arrays of 512-voxel bricks, brick b =
 // (bx*nby + by)*nbz + bz, brick-local voxel (x*8 + y)*8 + z.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -26,20 +27,24 @@ __global__ void k_fill3(float* t, float* w, float* c, size_t n) {
     }
 }
 
-// brick layout <-> C-order (X,Y,Z) of the shard.  TO_CORDER: dst C-order, src bricks.
+// brick layout <-> C-order rows of the shard: C-order row i of the buffer is local x row
+// rows[i] (rows == nullptr: row0 + i).  TO_CORDER: buffer <- bricks, else bricks <- buffer.
 template <bool TO_CORDER>
-__global__ void k_relayout(Vol v, const float* __restrict__ src, float* __restrict__ dst) {
-    const size_t n = (size_t)v.dims[0] * v.dims[1] * v.dims[2];
+__global__ void k_rows(Vol v, const long long* __restrict__ rows, long long row0, long long nrows,
+                       float* __restrict__ bricks, float* __restrict__ buf) {
+    const size_t yz = (size_t)v.dims[1] * v.dims[2];
+    const size_t n = (size_t)nrows * yz;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
         const int z = (int)(i % v.dims[2]);
-        const size_t xy = i / v.dims[2];
-        const int y = (int)(xy % v.dims[1]);
-        const int x = (int)(xy / v.dims[1]);
+        const size_t ry = i / v.dims[2];
+        const int y = (int)(ry % v.dims[1]);
+        const long long r = (long long)(ry / v.dims[1]);
+        const int x = (int)(rows ? rows[r] : row0 + r);
         const size_t b = ((size_t)(x >> 3) * v.nb[1] + (y >> 3)) * v.nb[2] + (z >> 3);
         const size_t j = b * kBrickVox + (size_t)((x & 7) * 8 + (y & 7)) * 8 + (z & 7);
-        if (TO_CORDER) dst[i] = src[j];
-        else dst[j] = src[i];
+        if (TO_CORDER) buf[i] = bricks[j];
+        else bricks[j] = buf[i];
     }
 }
 
@@ -208,35 +213,53 @@ int dense_flush(tsdf_dense* h) {
     return r;
 }
 
+// C-order get/set of the whole shard through a bounded device buffer (<= 64 MiB of rows at a time).
 int dense_xfer(tsdf_dense* h, float* tsdf_, float* weight_, float* color_, bool get) {
     Base& B = h->b;
     TSDF_TRY(dense_flush(h));
     TSDF_HIP(hipSetDevice(B.device));
-    const size_t n = (size_t)B.vol.dims[0] * B.vol.dims[1] * B.vol.dims[2];
+    const size_t yz = (size_t)B.vol.dims[1] * B.vol.dims[2];
+    const long long X = B.vol.dims[0];
+    const long long chunk = std::max<long long>(1, std::min<long long>(X, (64ll << 20) / (long long)(yz * sizeof(float))));
     float* tmp = nullptr;
-    TSDF_HIP(hipMalloc(&tmp, n * sizeof(float)));
+    TSDF_HIP(hipMalloc(&tmp, (size_t)chunk * yz * sizeof(float)));
     float* host[3] = {tsdf_, weight_, color_};
     float* dev[3] = {B.pool.tsdf, B.pool.weight, B.pool.color};
     hipError_t e = hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>(((size_t)chunk * yz + 255) / 256, (size_t)B.n_cu * 16);
     for (int k = 0; k < 3 && e == hipSuccess; ++k) {
         if (!host[k]) continue;
-        if (get) {
-            hipLaunchKernelGGL(k_relayout<true>, dim3(4096), dim3(256), 0, B.stream, B.vol, (const float*)dev[k], tmp);
-            e = hipGetLastError();
-            if (e == hipSuccess) e = hipMemcpyAsync(host[k], tmp, n * sizeof(float), hipMemcpyDeviceToHost, B.stream);
-        } else {
-            e = hipMemcpyAsync(tmp, host[k], n * sizeof(float), hipMemcpyHostToDevice, B.stream);
-            if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_relayout<false>, dim3(4096), dim3(256), 0, B.stream, B.vol, (const float*)tmp, dev[k]);
+        for (long long r0 = 0; r0 < X && e == hipSuccess; r0 += chunk) {
+            const long long nr = std::min(chunk, X - r0);
+            const size_t bytes = (size_t)nr * yz * sizeof(float);
+            if (get) {
+                hipLaunchKernelGGL(k_rows<true>, dim3(grid), dim3(256), 0, B.stream, B.vol, (const long long*)nullptr, r0,
+                                   nr, dev[k], tmp);
                 e = hipGetLastError();
+                if (e == hipSuccess) e = hipMemcpyAsync(host[k] + (size_t)r0 * yz, tmp, bytes, hipMemcpyDeviceToHost, B.stream);
+            } else {
+                e = hipMemcpyAsync(tmp, host[k] + (size_t)r0 * yz, bytes, hipMemcpyHostToDevice, B.stream);
+                if (e == hipSuccess) {
+                    hipLaunchKernelGGL(k_rows<false>, dim3(grid), dim3(256), 0, B.stream, B.vol, (const long long*)nullptr,
+                                       r0, nr, dev[k], tmp);
+                    e = hipGetLastError();
+                }
             }
+            if (e == hipSuccess) e = hipStreamSynchronize(B.stream);  // tmp is reused by the next chunk
         }
-        if (e == hipSuccess) e = hipStreamSynchronize(B.stream);
     }
     (void)hipFree(tmp);
     TSDF_HIP(e);
     return TSDF_OK;
 }
+
+struct DevPtrs {
+    std::vector<void*> p;
+    ~DevPtrs() {
+        for (void* q : p)
+            if (q) (void)hipFree(q);
+    }
+};
 
 }  // namespace
 
@@ -391,10 +414,50 @@ int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset) {
 }
 
 int tsdf_dense_extract_mesh(tsdf_dense_t* h, int64_t* n_verts, int64_t* n_tris) {
-    if (!h || !n_verts || !n_tris) return set_error(TSDF_E_ARG, "null pointer");
-    TSDF_HIP(hipSetDevice(h->b.device));
+    return tsdf_dense_extract_mesh_halo(h, 0, nullptr, 0, nullptr, nullptr, 0, n_verts, n_tris);
+}
+
+int tsdf_dense_mesh_halo_rows(tsdf_dense_t* h, int64_t global_x, int64_t* rows, int64_t* n_rows) {
+    if (!h || !n_rows) return set_error(TSDF_E_ARG, "null pointer");
+    std::vector<long long> v;
+    TSDF_TRY(mesh_halo_rows(h->b.vol, global_x, &v));
+    if (rows) {
+        if (*n_rows < (int64_t)v.size()) return set_error(TSDF_E_ARG, "rows holds %lld, need %zu", (long long)*n_rows, v.size());
+        for (size_t i = 0; i < v.size(); ++i) rows[i] = v[i];
+    }
+    *n_rows = (int64_t)v.size();
+    return TSDF_OK;
+}
+
+int tsdf_dense_extract_mesh_halo(tsdf_dense_t* h, int64_t global_x, const int64_t* halo_gx, int64_t n_halo,
+                                 const float* halo_tsdf, const float* halo_color, int flags, int64_t* n_verts,
+                                 int64_t* n_tris) {
+    if (!h || !n_verts || !n_tris || n_halo < 0 || (n_halo > 0 && (!halo_gx || !halo_tsdf || !halo_color)))
+        return set_error(TSDF_E_ARG, "bad arguments");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
     TSDF_TRY(dense_flush(h));
-    TSDF_TRY(extract_mesh(h->b, h->b.pool, h->mesh));
+    MeshDomain d;
+    TSDF_TRY(mesh_domain(B.vol, global_x, halo_gx, n_halo, &d));
+    const size_t hb = (size_t)n_halo * B.vol.dims[1] * B.vol.dims[2] * sizeof(float);
+    const float *ht = halo_tsdf, *hc = halo_color;
+    float *ut = nullptr, *uc = nullptr;
+    int r = TSDF_OK;
+    if (n_halo > 0 && !(flags & TSDF_DEVICE_PTRS)) {  // host halo rows: upload them for the call
+        hipError_t e = hipMalloc(&ut, hb);
+        if (e == hipSuccess) e = hipMalloc(&uc, hb);
+        if (e == hipSuccess) e = hipMemcpyAsync(ut, halo_tsdf, hb, hipMemcpyHostToDevice, B.stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(uc, halo_color, hb, hipMemcpyHostToDevice, B.stream);
+        if (e != hipSuccess) r = set_error(TSDF_E_HIP, "halo upload: %s", hipGetErrorString(e));
+        ht = ut;
+        hc = uc;
+    } else if (n_halo > 0) {
+        TSDF_HIP(hipDeviceSynchronize());  // the caller's producer (e.g. a collective) may be on another stream
+    }
+    if (r == TSDF_OK) r = extract_mesh(B, B.pool, h->mesh, d, ht, hc);
+    if (ut) (void)hipFree(ut);
+    if (uc) (void)hipFree(uc);
+    TSDF_TRY(r);
     *n_verts = h->mesh.n_verts;
     *n_tris = h->mesh.n_tris;
     return TSDF_OK;
@@ -404,6 +467,48 @@ int tsdf_dense_get_mesh(tsdf_dense_t* h, float* verts, float* normals, uint8_t* 
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));
     return copy_mesh(h->b, h->mesh, verts, normals, colors, faces);
+}
+
+int tsdf_dense_get_mesh_keys(tsdf_dense_t* h, int64_t* keys) {
+    if (!h || !keys) return set_error(TSDF_E_ARG, "null pointer");
+    TSDF_HIP(hipSetDevice(h->b.device));
+    return copy_mesh(h->b, h->mesh, nullptr, nullptr, nullptr, nullptr, keys);
+}
+
+int tsdf_dense_get_rows(tsdf_dense_t* h, const int64_t* rows, int64_t n_rows, float* tsdf_, float* weight_,
+                        float* color_, int flags) {
+    if (!h || n_rows < 0 || (n_rows > 0 && !rows)) return set_error(TSDF_E_ARG, "bad arguments");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(dense_flush(h));
+    if (n_rows == 0) return TSDF_OK;
+    for (int64_t i = 0; i < n_rows; ++i)
+        if (rows[i] < 0 || rows[i] >= B.vol.dims[0])
+            return set_error(TSDF_E_ARG, "local row %lld outside [0, %d)", (long long)rows[i], B.vol.dims[0]);
+    const size_t yz = (size_t)B.vol.dims[1] * B.vol.dims[2];
+    const size_t bytes = (size_t)n_rows * yz * sizeof(float);
+    DevPtrs bufs;
+    long long* drows = nullptr;
+    TSDF_HIP(hipMalloc(&drows, sizeof(long long) * n_rows));
+    bufs.p.push_back(drows);
+    TSDF_HIP(hipMemcpyAsync(drows, rows, sizeof(long long) * n_rows, hipMemcpyHostToDevice, B.stream));
+    float* out[3] = {tsdf_, weight_, color_};
+    float* dev[3] = {B.pool.tsdf, B.pool.weight, B.pool.color};
+    const unsigned grid = (unsigned)std::min<size_t>(((size_t)n_rows * yz + 255) / 256, (size_t)B.n_cu * 16);
+    for (int k = 0; k < 3; ++k) {
+        if (!out[k]) continue;
+        float* dst = out[k];
+        if (!(flags & TSDF_DEVICE_PTRS)) {
+            TSDF_HIP(hipMalloc(&dst, bytes));
+            bufs.p.push_back(dst);
+        }
+        hipLaunchKernelGGL(k_rows<true>, dim3(grid), dim3(256), 0, B.stream, B.vol, (const long long*)drows, 0ll,
+                           (long long)n_rows, dev[k], dst);
+        TSDF_HIP(hipGetLastError());
+        if (!(flags & TSDF_DEVICE_PTRS)) TSDF_HIP(hipMemcpyAsync(out[k], dst, bytes, hipMemcpyDeviceToHost, B.stream));
+    }
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    return TSDF_OK;
 }
 
 int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {

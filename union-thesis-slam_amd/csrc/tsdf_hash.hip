@@ -267,6 +267,54 @@ __global__ void k_to_dense(Vol v, Table t, Pool pool, float* ot, float* ow, floa
     }
 }
 
+// Live blocks out (one wave per slot): block coordinates, the 512 voxels of each field in the
+// brick-local order (x*8 + y)*8 + z, and the 8 entry words.  Output order = claim order.
+__global__ void k_export_blocks(Table t, Pool pool, unsigned long long* counter, long long cap, int* bxyz,
+                                float* ot, float* ow, float* oc, unsigned long long* oocc) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long s = wave; s < t.capacity; s += nw) {
+        const unsigned long long key = coh_load(&t.keys[s]);
+        if (key == kEmpty || key == kTomb) continue;
+        long long i = 0;
+        if (lane == 0) i = (long long)atomicAdd(counter, 1ull);
+        i = __shfl(i, 0);
+        if (i >= cap) continue;
+        const long long blk = coh_load(&t.vals[s]);
+        if (lane < 3) bxyz[3 * i + lane] = (int)((key >> (21 * lane)) & 0x1FFFFF);
+        if (lane < 8 && oocc) oocc[8 * i + lane] = coh_load(&t.occ[blk * 8 + lane]);
+        const size_t src = (size_t)blk * kBrickVox + (size_t)lane * 8, dst = (size_t)i * kBrickVox + (size_t)lane * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (ot) *(float4*)(ot + dst + 4 * h) = *(const float4*)(pool.tsdf + src + 4 * h);
+            if (ow) *(float4*)(ow + dst + 4 * h) = *(const float4*)(pool.weight + src + 4 * h);
+            if (oc) *(float4*)(oc + dst + 4 * h) = *(const float4*)(pool.color + src + 4 * h);
+        }
+    }
+}
+
+// Imported blocks in (one wave per block; blk from k_insert_blocks): contents and entry words
+// overwrite the block.
+__global__ void k_write_blocks(Table t, Pool pool, const int* blk, long long n, const float* it, const float* iw,
+                               const float* ic, const unsigned long long* iocc) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long i = wave; i < n; i += nw) {
+        const long long b = blk[i];
+        if (b < 0) continue;
+        if (lane < 8) coh_store(&t.occ[b * 8 + lane], iocc ? iocc[8 * i + lane] : ~0ull);
+        const size_t dst = (size_t)b * kBrickVox + (size_t)lane * 8, src = (size_t)i * kBrickVox + (size_t)lane * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (it) *(float4*)(pool.tsdf + dst + 4 * h) = *(const float4*)(it + src + 4 * h);
+            if (iw) *(float4*)(pool.weight + dst + 4 * h) = *(const float4*)(iw + src + 4 * h);
+            if (ic) *(float4*)(pool.color + dst + 4 * h) = *(const float4*)(ic + src + 4 * h);
+        }
+    }
+}
+
 __global__ void k_fill_dense(float* t, float* w, float* c, size_t n) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
@@ -654,6 +702,39 @@ int upload(tsdf_hash* h, const void* src, size_t bytes, void** dst) {
     return TSDF_OK;
 }
 
+// Find-or-insert of distinct block keys (room first: the reference resizes before inserting,
+// hash_fusion.py:208-209); *dblk / *dslot: device arrays (owned by bufs) of each key's block and
+// slot.  Stream-ordered: the caller's kernels that use them follow on the handle's stream.
+int insert_block_keys(tsdf_hash* h, const std::vector<unsigned long long>& keys, DevBufs& bufs, void** dblk,
+                      void** dslot) {
+    Base& B = h->b;
+    const long long nk = (long long)keys.size();
+    TSDF_TRY(read_state(h));
+    InfoDev inf{};
+    TSDF_TRY(info_raw(h, &inf));
+    while ((double)(inf.used + inf.tomb + nk) >= 0.75 * (double)h->t.capacity) {
+        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+        TSDF_TRY(info_raw(h, &inf));
+    }
+    if (h->host_st.pool_top + nk > h->t.max_blocks - h->host_st.free_count)
+        TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * nk)));
+    void* dkeys;
+    TSDF_TRY(upload(h, keys.data(), sizeof(unsigned long long) * nk, &dkeys));
+    bufs.add(dkeys);
+    TSDF_HIP(hipMalloc(dblk, sizeof(int) * (nk ? nk : 1)));
+    bufs.add(*dblk);
+    TSDF_HIP(hipMalloc(dslot, sizeof(long long) * (nk ? nk : 1)));
+    bufs.add(*dslot);
+    if (nk == 0) return TSDF_OK;
+    hipLaunchKernelGGL(k_insert_blocks, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, B.stream, h->t,
+                       B.pool, (const unsigned long long*)dkeys, (long long)nk, (int*)*dblk, (long long*)*dslot);
+    TSDF_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
+                       (PoolReport*)nullptr, -1ll);
+    TSDF_HIP(hipGetLastError());
+    return TSDF_OK;
+}
+
 // unique packed block keys of the in-volume voxels of ijk
 std::vector<unsigned long long> unique_blocks(const Vol& v, const int64_t* ijk, int64_t n) {
     std::vector<unsigned long long> keys;
@@ -831,30 +912,9 @@ int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float*
     TSDF_TRY(hash_flush(h));
     std::vector<unsigned long long> keys = unique_blocks(v, ijk, n);
     const long long nk = (long long)keys.size();
-    // room first (the reference resizes before inserting, hash_fusion.py:208-209)
-    TSDF_TRY(read_state(h));
-    InfoDev inf{};
-    TSDF_TRY(info_raw(h, &inf));
-    while ((double)(inf.used + inf.tomb + nk) >= 0.75 * (double)h->t.capacity) {
-        TSDF_TRY(resize_table(h, h->t.capacity * 2));
-        TSDF_TRY(info_raw(h, &inf));
-    }
-    if (h->host_st.pool_top + nk > h->t.max_blocks - h->host_st.free_count)
-        TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * nk)));
     DevBufs bufs;
-    void *dkeys, *dblk = nullptr, *dslot = nullptr, *dijk, *dt, *dw, *dc;
-    TSDF_TRY(upload(h, keys.data(), sizeof(unsigned long long) * nk, &dkeys));
-    bufs.add(dkeys);
-    TSDF_HIP(hipMalloc(&dblk, sizeof(int) * nk));
-    bufs.add(dblk);
-    TSDF_HIP(hipMalloc(&dslot, sizeof(long long) * nk));
-    bufs.add(dslot);
-    hipLaunchKernelGGL(k_insert_blocks, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, B.stream, h->t,
-                       B.pool, (const unsigned long long*)dkeys, (long long)nk, (int*)dblk, (long long*)dslot);
-    TSDF_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
-                       (PoolReport*)nullptr, -1ll);
-    TSDF_HIP(hipGetLastError());
+    void *dblk = nullptr, *dslot = nullptr, *dijk, *dt, *dw, *dc;
+    TSDF_TRY(insert_block_keys(h, keys, bufs, &dblk, &dslot));
     TSDF_TRY(upload(h, ijk, sizeof(int64_t) * 3 * n, &dijk));
     bufs.add(dijk);
     TSDF_TRY(upload(h, tsdf_, tsdf_ ? sizeof(float) * n : 0, &dt));
@@ -988,6 +1048,108 @@ int tsdf_hash_set_profiling(tsdf_hash_t* h, int on) {
     TSDF_HIP(hipSetDevice(h->b.device));
     TSDF_TRY(hash_flush(h));
     return h->b.set_profiling(on);
+}
+
+// Sparse export / import of whole blocks (the multi-GPU merge of bucket-range shards, DESIGN.md
+// §6): only live blocks move, never the dense extent.
+int tsdf_hash_export_blocks(tsdf_hash_t* h, int32_t* bxyz, float* tsdf_, float* weight_, float* color_,
+                            uint64_t* occ, int64_t* n_blocks, int flags) {
+    if (!h || !n_blocks) return set_error(TSDF_E_ARG, "null pointer");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
+    InfoDev inf{};
+    TSDF_TRY(info_raw(h, &inf));
+    const long long live = (long long)inf.used;
+    if (!bxyz) {  // count only
+        *n_blocks = live;
+        return TSDF_OK;
+    }
+    if (*n_blocks < live) return set_error(TSDF_E_ARG, "output holds %lld blocks, %lld live", (long long)*n_blocks, live);
+    const bool dev = (flags & TSDF_DEVICE_PTRS) != 0;
+    DevBufs bufs;
+    void* d[5] = {bxyz, tsdf_, weight_, color_, occ};
+    const size_t sz[5] = {sizeof(int32_t) * 3, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
+                          sizeof(float) * kBrickVox, sizeof(uint64_t) * 8};
+    if (!dev)
+        for (int k = 0; k < 5; ++k)
+            if (d[k]) {
+                TSDF_HIP(hipMalloc(&d[k], sz[k] * (live ? live : 1)));
+                bufs.add(d[k]);
+            }
+    unsigned long long* counter;
+    TSDF_HIP(hipMalloc(&counter, sizeof(unsigned long long)));
+    bufs.add(counter);
+    TSDF_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), B.stream));
+    hipLaunchKernelGGL(k_export_blocks, dim3(2048), dim3(256), 0, B.stream, h->t, B.pool, counter, live, (int*)d[0],
+                       (float*)d[1], (float*)d[2], (float*)d[3], (unsigned long long*)d[4]);
+    TSDF_HIP(hipGetLastError());
+    unsigned long long got = 0;
+    TSDF_HIP(hipMemcpyAsync(&got, counter, sizeof(got), hipMemcpyDeviceToHost, B.stream));
+    if (!dev) {
+        void* out[5] = {bxyz, tsdf_, weight_, color_, occ};
+        for (int k = 0; k < 5; ++k)
+            if (out[k]) TSDF_HIP(hipMemcpyAsync(out[k], d[k], sz[k] * live, hipMemcpyDeviceToHost, B.stream));
+    }
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    if ((long long)got != live) return set_error(TSDF_E_HIP, "exported %llu blocks, expected %lld", got, live);
+    *n_blocks = live;
+    return TSDF_OK;
+}
+
+int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_blocks, const float* tsdf_,
+                            const float* weight_, const float* color_, const uint64_t* occ, int flags) {
+    if (!h || n_blocks < 0 || (n_blocks > 0 && !bxyz)) return set_error(TSDF_E_ARG, "bad arguments");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
+    if (n_blocks == 0) return TSDF_OK;
+    const bool dev = (flags & TSDF_DEVICE_PTRS) != 0;
+    std::vector<int32_t> hb((size_t)n_blocks * 3);
+    if (dev) {
+        TSDF_HIP(hipDeviceSynchronize());  // the caller's producer may be on another stream
+        TSDF_HIP(hipMemcpy(hb.data(), bxyz, hb.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    } else {
+        std::memcpy(hb.data(), bxyz, hb.size() * sizeof(int32_t));
+    }
+    std::vector<unsigned long long> keys((size_t)n_blocks);
+    for (int64_t i = 0; i < n_blocks; ++i) {
+        const int bx = hb[3 * i], by = hb[3 * i + 1], bz = hb[3 * i + 2];
+        if (bx < 0 || by < 0 || bz < 0 || bx >= B.vol.nb[0] || by >= B.vol.nb[1] || bz >= B.vol.nb[2])
+            return set_error(TSDF_E_ARG, "block (%d,%d,%d) outside the volume", bx, by, bz);
+        keys[i] = pack_key(bx, by, bz);
+    }
+    {
+        std::vector<unsigned long long> u(keys);
+        std::sort(u.begin(), u.end());
+        if (std::adjacent_find(u.begin(), u.end()) != u.end()) return set_error(TSDF_E_ARG, "duplicate block in import");
+    }
+    DevBufs bufs;
+    void *dblk = nullptr, *dslot = nullptr;
+    TSDF_TRY(insert_block_keys(h, keys, bufs, &dblk, &dslot));
+    const void* in[4] = {tsdf_, weight_, color_, occ};
+    const size_t sz[4] = {sizeof(float) * kBrickVox, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
+                          sizeof(uint64_t) * 8};
+    void* d[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int k = 0; k < 4; ++k) {
+        if (!in[k]) continue;
+        if (dev) {
+            d[k] = (void*)in[k];
+        } else {
+            TSDF_TRY(upload(h, in[k], sz[k] * n_blocks, &d[k]));
+            bufs.add(d[k]);
+        }
+    }
+    hipLaunchKernelGGL(k_write_blocks, dim3(2048), dim3(256), 0, B.stream, h->t, B.pool, (const int*)dblk,
+                       (long long)n_blocks, (const float*)d[0], (const float*)d[1], (const float*)d[2],
+                       (const unsigned long long*)d[3]);
+    TSDF_HIP(hipGetLastError());
+    std::vector<int> blk((size_t)n_blocks);
+    TSDF_HIP(hipMemcpyAsync(blk.data(), dblk, sizeof(int) * n_blocks, hipMemcpyDeviceToHost, B.stream));
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    for (int64_t i = 0; i < n_blocks; ++i)
+        if (blk[i] < 0) return set_error(TSDF_E_CAPACITY, "hash import failed (table or pool full)");
+    return TSDF_OK;
 }
 
 }  // extern "C"

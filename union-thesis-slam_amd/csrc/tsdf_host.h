@@ -165,11 +165,23 @@ struct Mesh {
     float* normals = nullptr;         // n_verts x 3 unit normals (to positive tsdf)
     unsigned char* colors = nullptr;  // n_verts x 3 uint8 r, g, b
     int* faces = nullptr;             // n_tris x 3 vertex ids
+    long long* keys = nullptr;        // n_verts global vertex keys ((x*Y + y)*Z + z)*3 + axis
     long long n_verts = 0, n_tris = 0;
     void release();
 };
-int extract_mesh(Base& B, const Pool& pool, Mesh& m);
-int copy_mesh(Base& B, const Mesh& m, float* verts, float* normals, uint8_t* colors, int32_t* faces);
+// The global x rows marching cubes runs over for one shard (tsdf_mesh.hip, Grid).
+struct MeshDomain {
+    int xlo = 0, xhi = 0;
+    std::vector<int> row_map;               // [xhi - xlo]: local row, -2 - halo index, or -1
+    std::vector<int> vrow_gx;               // vertex rows (local rows and cap rows), increasing x
+    std::vector<unsigned char> vrow_cap;
+};
+// global_x > 0: the unsharded volume's x extent, halo rows given; 0: the shard alone
+int mesh_domain(const Vol& v, long long global_x, const int64_t* halo_gx, long long n_halo, MeshDomain* d);
+int mesh_halo_rows(const Vol& v, long long global_x, std::vector<long long>* out);
+int extract_mesh(Base& B, const Pool& pool, Mesh& m, const MeshDomain& d, const float* ht, const float* hc);
+int copy_mesh(Base& B, const Mesh& m, float* verts, float* normals, uint8_t* colors, int32_t* faces,
+              int64_t* keys = nullptr);
 
 // end_call on every exit path of an integrate call (error returns included).
 struct CallGuard {

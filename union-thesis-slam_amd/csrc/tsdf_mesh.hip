@@ -115,34 +115,56 @@ __device__ inline void edge_anchor(int e, int& off, int& axis) {
     off = ((r & 1) << u) | (((r >> 1) & 1) << v);
 }
 
+// The volume as marching cubes sees it: rows of constant global x.  Local rows live in the
+// handle's brick pool; rows owned by other shards (halo rows, exchanged by the caller) arrive as
+// C-order (Y, Z) slices.  row_map[gx - xlo] says where global row gx is: >= 0 local row,
+// <= -2 halo row -2-r, -1 absent.  Marching cubes runs over the global x range [xlo, xhi):
+// gradients clamp there, x-edges and cells need gx + 1 < xhi.  A shard's "vertex rows" are its
+// local rows plus each cap row (a halo row gx whose gx - 1 is local): the cells a shard owns are
+// those anchored at its local rows, and a cap row carries the y/z-edge vertices of their +x faces
+// (duplicates of the next shard's own vertices, identified by the same global key).
 struct Grid {
-    int X, Y, Z;       // local voxels
-    int nby, nbz;      // bricks per axis (y, z)
-    const float* t;    // brick-layout state
+    int Y, Z;
+    int xlo, xhi;
+    int nby, nbz;              // brick geometry of the local rows
+    const int* row_map;        // [xhi - xlo]
+    const int* vrow_gx;        // [nrows] global x of the vertex rows, increasing
+    const unsigned char* vrow_cap;  // [nrows] 1: cap row (y/z-edge vertices only, no cells)
+    const float* t;            // brick-layout state (local rows)
     const float* c;
+    const float* ht;           // halo rows, C-order [n_halo][Y][Z]
+    const float* hc;
 };
 
-__device__ inline size_t brick_addr(const Grid& g, int x, int y, int z) {
-    const size_t b = ((size_t)(x >> 3) * g.nby + (y >> 3)) * g.nbz + (z >> 3);
-    return b * kBrickVox + (size_t)(((x & 7) * 8 + (y & 7)) * 8 + (z & 7));
+__device__ inline float gval(const Grid& g, const float* brick, const float* halo, int gx, int y, int z) {
+    const int r = g.row_map[gx - g.xlo];
+    if (r >= 0) {
+        const size_t b = ((size_t)(r >> 3) * g.nby + (y >> 3)) * g.nbz + (z >> 3);
+        return brick[b * kBrickVox + (size_t)(((r & 7) * 8 + (y & 7)) * 8 + (z & 7))];
+    }
+    return halo[((size_t)(-2 - r) * g.Y + y) * g.Z + z];
 }
-__device__ inline float tval(const Grid& g, int x, int y, int z) { return g.t[brick_addr(g, x, y, z)]; }
+__device__ inline float tval(const Grid& g, int gx, int y, int z) { return gval(g, g.t, g.ht, gx, y, z); }
+__device__ inline float cval(const Grid& g, int gx, int y, int z) { return gval(g, g.c, g.hc, gx, y, z); }
 
-__global__ void k_mc_classify(Grid g, const unsigned char* __restrict__ ntri, unsigned char* __restrict__ ebits,
-                              unsigned char* __restrict__ cubes, unsigned* __restrict__ vcnt,
-                              unsigned* __restrict__ tcnt) {
-    const size_t n = (size_t)g.X * g.Y * g.Z;
+__global__ void k_mc_classify(Grid g, int nrows, const unsigned char* __restrict__ ntri,
+                              unsigned char* __restrict__ ebits, unsigned char* __restrict__ cubes,
+                              unsigned* __restrict__ vcnt, unsigned* __restrict__ tcnt) {
+    const size_t n = (size_t)nrows * g.Y * g.Z;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const int z = (int)(i % g.Z);
         const size_t xy = i / g.Z;
-        const int y = (int)(xy % g.Y), x = (int)(xy / g.Y);
+        const int y = (int)(xy % g.Y), row = (int)(xy / g.Y);
+        const int x = g.vrow_gx[row];
+        const bool cap = g.vrow_cap[row] != 0;
         const bool in0 = tval(g, x, y, z) < 0.0f;
+        const bool xn = !cap && x + 1 < g.xhi;  // x-edge and cells only from local rows
         unsigned bits = 0;
-        if (x + 1 < g.X && (tval(g, x + 1, y, z) < 0.0f) != in0) bits |= 1u;
+        if (xn && (tval(g, x + 1, y, z) < 0.0f) != in0) bits |= 1u;
         if (y + 1 < g.Y && (tval(g, x, y + 1, z) < 0.0f) != in0) bits |= 2u;
         if (z + 1 < g.Z && (tval(g, x, y, z + 1) < 0.0f) != in0) bits |= 4u;
         unsigned cube = 0, nt = 0;
-        if (x + 1 < g.X && y + 1 < g.Y && z + 1 < g.Z) {
+        if (xn && y + 1 < g.Y && z + 1 < g.Z) {
 #pragma unroll
             for (int c = 0; c < 8; ++c)
                 cube |= (unsigned)(tval(g, x + (c & 1), y + ((c >> 1) & 1), z + ((c >> 2) & 1)) < 0.0f) << c;
@@ -155,23 +177,25 @@ __global__ void k_mc_classify(Grid g, const unsigned char* __restrict__ ntri, un
     }
 }
 
-// central-difference gradient of the tsdf at a voxel (indices clamped at the volume's faces)
+// central-difference gradient of the tsdf at a voxel (indices clamped at the faces of the
+// meshed range)
 __device__ inline void grad(const Grid& g, int x, int y, int z, float out[3]) {
-    out[0] = tval(g, min(x + 1, g.X - 1), y, z) - tval(g, max(x - 1, 0), y, z);
+    out[0] = tval(g, min(x + 1, g.xhi - 1), y, z) - tval(g, max(x - 1, g.xlo), y, z);
     out[1] = tval(g, x, min(y + 1, g.Y - 1), z) - tval(g, x, max(y - 1, 0), z);
     out[2] = tval(g, x, y, min(z + 1, g.Z - 1)) - tval(g, x, y, max(z - 1, 0));
 }
 
-__global__ void k_mc_vertices(Grid g, const unsigned char* __restrict__ ebits, const unsigned* __restrict__ vbase,
-                              float ox, float oy, float oz, float vs, float* __restrict__ verts,
-                              float* __restrict__ normals, unsigned char* __restrict__ colors) {
-    const size_t n = (size_t)g.X * g.Y * g.Z;
+__global__ void k_mc_vertices(Grid g, int nrows, const unsigned char* __restrict__ ebits,
+                              const unsigned* __restrict__ vbase, float ox, float oy, float oz, float vs,
+                              float* __restrict__ verts, float* __restrict__ normals,
+                              unsigned char* __restrict__ colors, long long* __restrict__ keys) {
+    const size_t n = (size_t)nrows * g.Y * g.Z;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const unsigned bits = ebits[i];
         if (!bits) continue;
         const int z = (int)(i % g.Z);
         const size_t xy = i / g.Z;
-        const int y = (int)(xy % g.Y), x = (int)(xy / g.Y);
+        const int y = (int)(xy % g.Y), x = g.vrow_gx[xy / g.Y];
         const float v1 = tval(g, x, y, z);
         float g1[3];
         grad(g, x, y, z, g1);
@@ -195,36 +219,41 @@ __global__ void k_mc_vertices(Grid g, const unsigned char* __restrict__ ebits, c
             }
             // grid_fusion.py:336-346: colour of the voxel at round(verts), decoded to uint8
             const int rx = (int)rintf(p[0]), ry = (int)rintf(p[1]), rz = (int)rintf(p[2]);
-            const float cv = g.c[brick_addr(g, rx, ry, rz)];
+            const float cv = cval(g, rx, ry, rz);
             const float cb = floorf(cv / 65536.0f);
             const float cg = floorf((cv - cb * 65536.0f) / 256.0f);
             const float cr = cv - cb * 65536.0f - cg * 256.0f;
             colors[3 * (size_t)id + 0] = (unsigned char)(int)floorf(cr);
             colors[3 * (size_t)id + 1] = (unsigned char)(int)floorf(cg);
             colors[3 * (size_t)id + 2] = (unsigned char)(int)floorf(cb);
+            // global identity of the vertex: (voxel, axis) in the unsharded volume's C-order
+            keys[id] = ((((long long)x * g.Y) + y) * g.Z + z) * 3 + a;
             ++id;
         }
     }
 }
 
-__global__ void k_mc_triangles(Grid g, const signed char* __restrict__ tri, const unsigned char* __restrict__ cubes,
-                               const unsigned char* __restrict__ ebits, const unsigned* __restrict__ vbase,
-                               const unsigned* __restrict__ tbase, int* __restrict__ faces) {
-    const size_t n = (size_t)g.X * g.Y * g.Z;
+__global__ void k_mc_triangles(Grid g, int nrows, const signed char* __restrict__ tri,
+                               const unsigned char* __restrict__ cubes, const unsigned char* __restrict__ ebits,
+                               const unsigned* __restrict__ vbase, const unsigned* __restrict__ tbase,
+                               int* __restrict__ faces) {
+    const size_t n = (size_t)nrows * g.Y * g.Z;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const unsigned cube = cubes[i];
         if (cube == 0 || cube == 255) continue;
         const int z = (int)(i % g.Z);
         const size_t xy = i / g.Z;
-        const int y = (int)(xy % g.Y), x = (int)(xy / g.Y);
+        const int y = (int)(xy % g.Y), row = (int)(xy / g.Y);
         size_t f = tbase[i];
-        const signed char* row = tri + 16 * cube;
-        for (int k = 0; row[k] >= 0; k += 3) {
+        const signed char* rowt = tri + 16 * cube;
+        for (int k = 0; rowt[k] >= 0; k += 3) {
             int vid[3];
             for (int j = 0; j < 3; ++j) {
                 int off, axis;
-                edge_anchor(row[k + j], off, axis);
-                const size_t e = (((size_t)(x + (off & 1)) * g.Y + (y + ((off >> 1) & 1))) * g.Z) + (z + ((off >> 2) & 1));
+                edge_anchor(rowt[k + j], off, axis);
+                // the vertex row after a local row is global x + 1 (local or cap)
+                const size_t e = (((size_t)(row + (off & 1)) * g.Y + (y + ((off >> 1) & 1))) * g.Z) +
+                                 (z + ((off >> 2) & 1));
                 const unsigned bits = ebits[e];
                 vid[j] = (int)(vbase[e] + (unsigned)__popc(bits & ((1u << axis) - 1u)));
             }
@@ -249,51 +278,137 @@ int dev_alloc(T** p, size_t n) {
 namespace tsdf {
 
 void Mesh::release() {
-    for (void* p : {(void*)verts, (void*)normals, (void*)colors, (void*)faces})
+    for (void* p : {(void*)verts, (void*)normals, (void*)colors, (void*)faces, (void*)keys})
         if (p) (void)hipFree(p);
     verts = normals = nullptr;
     colors = nullptr;
     faces = nullptr;
+    keys = nullptr;
     n_verts = n_tris = 0;
 }
 
-// Extract into m (device buffers) from a brick-layout volume of local dims X, Y, Z.
-int extract_mesh(Base& B, const Pool& pool, Mesh& m) {
+int mesh_domain(const Vol& v, long long global_x, const int64_t* halo_gx, long long n_halo, MeshDomain* d) {
+    const int nl = v.dims[0];
+    auto gx_of = [&](int lr) { return v.off[0] + (lr >> 3) * v.xstride + (lr & 7); };
+    if (global_x > 0) {
+        d->xlo = 0;
+        d->xhi = (int)global_x;
+    } else {  // the shard alone: its own rows must be contiguous
+        if (v.xstride != kBrickEdge && v.nb[0] > 1)
+            return set_error(TSDF_E_ARG, "a cyclic column shard is meshed with its neighbours' border rows "
+                                         "(tsdf_dense_extract_mesh_halo)");
+        d->xlo = gx_of(0);
+        d->xhi = gx_of(nl - 1) + 1;
+    }
+    const int span = d->xhi - d->xlo;
+    if (span <= 0 || global_x > (1 << 24)) return set_error(TSDF_E_ARG, "bad global x extent %lld", global_x);
+    d->row_map.assign(span, -1);
+    for (int lr = 0; lr < nl; ++lr) {
+        const int gx = gx_of(lr);
+        if (gx < d->xlo || gx >= d->xhi) return set_error(TSDF_E_ARG, "local row %d (x %d) outside [%d, %d)", lr, gx, d->xlo, d->xhi);
+        d->row_map[gx - d->xlo] = lr;
+    }
+    for (long long h = 0; h < n_halo; ++h) {
+        const long long gx = halo_gx[h];
+        if (gx < d->xlo || gx >= d->xhi) return set_error(TSDF_E_ARG, "halo row %lld outside [%d, %d)", gx, d->xlo, d->xhi);
+        if (d->row_map[gx - d->xlo] >= 0) return set_error(TSDF_E_ARG, "halo row %lld is a local row", gx);
+        if (d->row_map[gx - d->xlo] <= -2) return set_error(TSDF_E_ARG, "halo row %lld given twice", gx);
+        d->row_map[gx - d->xlo] = (int)(-2 - h);
+    }
+    auto present = [&](long long gx) { return gx < d->xlo || gx >= d->xhi || d->row_map[gx - d->xlo] != -1; };
+    d->vrow_gx.clear();
+    d->vrow_cap.clear();
+    for (int gx = d->xlo; gx < d->xhi; ++gx) {
+        const int r = d->row_map[gx - d->xlo];
+        const bool local = r >= 0, prev_local = gx > d->xlo && d->row_map[gx - 1 - d->xlo] >= 0;
+        if (!local && !prev_local) continue;
+        // every row the cells and gradients read: x - 1, x + 1 (and x + 1 of a cap row)
+        if (!present(gx) || !present(gx - 1) || !present(gx + 1))
+            return set_error(TSDF_E_ARG, "mesh of x row %d needs rows %d..%d: pass the missing border rows "
+                                         "(tsdf_dense_mesh_halo_rows)", gx, gx - 1, gx + 1);
+        d->vrow_gx.push_back(gx);
+        d->vrow_cap.push_back(local ? 0 : 1);
+    }
+    return TSDF_OK;
+}
+
+int mesh_halo_rows(const Vol& v, long long global_x, std::vector<long long>* out) {
+    out->clear();
+    if (global_x <= 0 || global_x > (1 << 24)) return set_error(TSDF_E_ARG, "bad global x extent %lld", global_x);
+    std::vector<char> local((size_t)global_x, 0);
+    for (int lr = 0; lr < v.dims[0]; ++lr) {
+        const long long gx = v.off[0] + (long long)(lr >> 3) * v.xstride + (lr & 7);
+        if (gx >= global_x) return set_error(TSDF_E_ARG, "local row at x %lld beyond the global extent", gx);
+        local[gx] = 1;
+    }
+    std::vector<char> need((size_t)global_x, 0);
+    for (long long gx = 0; gx < global_x; ++gx) {
+        if (!local[gx]) continue;
+        if (gx - 1 >= 0) need[gx - 1] = 1;
+        if (gx + 1 < global_x) need[gx + 1] = 1;
+        if (gx + 2 < global_x && !local[gx + 1]) need[gx + 2] = 1;  // gradient of the cap row
+    }
+    for (long long gx = 0; gx < global_x; ++gx)
+        if (need[gx] && !local[gx]) out->push_back(gx);
+    return TSDF_OK;
+}
+
+// Extract into m (device buffers): the cells anchored at the shard's local rows over the range
+// and halo rows of `d` (halo rows: device C-order slices, nullptr when there are none).
+int extract_mesh(Base& B, const Pool& pool, Mesh& m, const MeshDomain& d, const float* ht, const float* hc) {
     m.release();
     const McTable& tab = table();
+    const int nrows = (int)d.vrow_gx.size();
     Grid g;
-    g.X = B.vol.dims[0];
     g.Y = B.vol.dims[1];
     g.Z = B.vol.dims[2];
+    g.xlo = d.xlo;
+    g.xhi = d.xhi;
     g.nby = B.vol.nb[1];
     g.nbz = B.vol.nb[2];
     g.t = pool.tsdf;
     g.c = pool.color;
-    const size_t n = (size_t)g.X * g.Y * g.Z;
+    g.ht = ht;
+    g.hc = hc;
+    const size_t n = (size_t)nrows * g.Y * g.Z;
     if (n >= (1ull << 31)) return set_error(TSDF_E_ARG, "volume too large for one mesh extraction (>= 2^31 voxels)");
     hipStream_t s = B.stream;
-    unsigned char *ebits = nullptr, *cubes = nullptr, *ntri = nullptr;
+    unsigned char *ebits = nullptr, *cubes = nullptr, *ntri = nullptr, *vcap = nullptr;
     signed char* dtri = nullptr;
     unsigned *vcnt = nullptr, *tcnt = nullptr, *vbase = nullptr, *tbase = nullptr;
+    int *rmap = nullptr, *vgx = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int r = TSDF_OK;
     auto cleanup = [&]() {
         for (void* p : {(void*)ebits, (void*)cubes, (void*)ntri, (void*)dtri, (void*)vcnt, (void*)tcnt, (void*)vbase,
-                        (void*)tbase, tmp})
+                        (void*)tbase, (void*)rmap, (void*)vgx, (void*)vcap, tmp})
             if (p) (void)hipFree(p);
     };
     do {
         if ((r = dev_alloc(&ebits, n)) || (r = dev_alloc(&cubes, n)) || (r = dev_alloc(&ntri, 256)) ||
             (r = dev_alloc(&dtri, 256 * 16)) || (r = dev_alloc(&vcnt, n)) || (r = dev_alloc(&tcnt, n)) ||
-            (r = dev_alloc(&vbase, n + 1)) || (r = dev_alloc(&tbase, n + 1)))
+            (r = dev_alloc(&vbase, n + 1)) || (r = dev_alloc(&tbase, n + 1)) ||
+            (r = dev_alloc(&rmap, d.row_map.size())) || (r = dev_alloc(&vgx, (size_t)nrows)) ||
+            (r = dev_alloc(&vcap, (size_t)nrows)))
             break;
         hipError_t e = hipMemcpyAsync(ntri, tab.ntri, 256, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(dtri, tab.tri, 256 * 16, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(rmap, d.row_map.data(), sizeof(int) * d.row_map.size(), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && nrows) e = hipMemcpyAsync(vgx, d.vrow_gx.data(), sizeof(int) * nrows, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && nrows) e = hipMemcpyAsync(vcap, d.vrow_cap.data(), nrows, hipMemcpyHostToDevice, s);
+        g.row_map = rmap;
+        g.vrow_gx = vgx;
+        g.vrow_cap = vcap;
+        if (n == 0) {
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) r = set_error(TSDF_E_HIP, "mesh setup: %s", hipGetErrorString(e));
+            break;
+        }
         const unsigned grid = (unsigned)std::min<size_t>((n + 255) / 256, (size_t)B.n_cu * 32);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_mc_classify, dim3(grid), dim3(256), 0, s, g, (const unsigned char*)ntri, ebits, cubes,
-                               vcnt, tcnt);
+            hipLaunchKernelGGL(k_mc_classify, dim3(grid), dim3(256), 0, s, g, nrows, (const unsigned char*)ntri, ebits,
+                               cubes, vcnt, tcnt);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, vcnt, vbase, (int)n, s);
@@ -313,12 +428,13 @@ int extract_mesh(Base& B, const Pool& pool, Mesh& m) {
         m.n_verts = (long long)last[0] + last[1];
         m.n_tris = (long long)last[2] + last[3];
         if ((r = dev_alloc(&m.verts, 3 * m.n_verts)) || (r = dev_alloc(&m.normals, 3 * m.n_verts)) ||
-            (r = dev_alloc(&m.colors, 3 * m.n_verts)) || (r = dev_alloc(&m.faces, 3 * m.n_tris)))
+            (r = dev_alloc(&m.colors, 3 * m.n_verts)) || (r = dev_alloc(&m.faces, 3 * m.n_tris)) ||
+            (r = dev_alloc(&m.keys, m.n_verts)))
             break;
-        hipLaunchKernelGGL(k_mc_vertices, dim3(grid), dim3(256), 0, s, g, (const unsigned char*)ebits,
+        hipLaunchKernelGGL(k_mc_vertices, dim3(grid), dim3(256), 0, s, g, nrows, (const unsigned char*)ebits,
                            (const unsigned*)vbase, B.vol.origin[0], B.vol.origin[1], B.vol.origin[2],
-                           (float)B.vol.vs, m.verts, m.normals, m.colors);
-        hipLaunchKernelGGL(k_mc_triangles, dim3(grid), dim3(256), 0, s, g, (const signed char*)dtri,
+                           (float)B.vol.vs, m.verts, m.normals, m.colors, m.keys);
+        hipLaunchKernelGGL(k_mc_triangles, dim3(grid), dim3(256), 0, s, g, nrows, (const signed char*)dtri,
                            (const unsigned char*)cubes, (const unsigned char*)ebits, (const unsigned*)vbase,
                            (const unsigned*)tbase, m.faces);
         e = hipGetLastError();
@@ -330,8 +446,10 @@ int extract_mesh(Base& B, const Pool& pool, Mesh& m) {
     return r;
 }
 
-int copy_mesh(Base& B, const Mesh& m, float* verts, float* normals, uint8_t* colors, int32_t* faces) {
+int copy_mesh(Base& B, const Mesh& m, float* verts, float* normals, uint8_t* colors, int32_t* faces,
+              int64_t* keys) {
     hipStream_t s = B.stream;
+    if (keys) TSDF_HIP(hipMemcpyAsync(keys, m.keys, sizeof(long long) * m.n_verts, hipMemcpyDeviceToHost, s));
     if (verts) TSDF_HIP(hipMemcpyAsync(verts, m.verts, sizeof(float) * 3 * m.n_verts, hipMemcpyDeviceToHost, s));
     if (normals) TSDF_HIP(hipMemcpyAsync(normals, m.normals, sizeof(float) * 3 * m.n_verts, hipMemcpyDeviceToHost, s));
     if (colors) TSDF_HIP(hipMemcpyAsync(colors, m.colors, 3 * m.n_verts, hipMemcpyDeviceToHost, s));

@@ -70,6 +70,10 @@ SIGNATURES = {
     "tsdf_dense_create_shard": [_P, _I, _I, _P, _D, _D, _I, _P],
     "tsdf_dense_extract_mesh": [_P, _P, _P],
     "tsdf_dense_get_mesh": [_P, _P, _P, _P, _P],
+    "tsdf_dense_mesh_halo_rows": [_P, _I64, _P, _P],
+    "tsdf_dense_extract_mesh_halo": [_P, _I64, _P, _I64, _P, _P, _I, _P, _P],
+    "tsdf_dense_get_mesh_keys": [_P, _P],
+    "tsdf_dense_get_rows": [_P, _P, _I64, _P, _P, _P, _I],
     "tsdf_mc_table": [_P, _P],
     "tsdf_frustum_bounds": [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P],
     "tsdf_dense_destroy": [_P],
@@ -92,6 +96,8 @@ SIGNATURES = {
     "tsdf_hash_resize": [_P, _I64],
     "tsdf_hash_info": [_P, _P],
     "tsdf_hash_get_dense": [_P, _P, _P, _P],
+    "tsdf_hash_export_blocks": [_P, _P, _P, _P, _P, _P, _P, _I],
+    "tsdf_hash_import_blocks": [_P, _P, _I64, _P, _P, _P, _P, _I],
     "tsdf_hash_sync": [_P],
     "tsdf_hash_stats": [_P, _P, _I],
     "tsdf_hash_set_profiling": [_P, _I],

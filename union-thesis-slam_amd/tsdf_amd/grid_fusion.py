@@ -204,17 +204,62 @@ class TSDFVolume:
     def reset(self):
         _ffi.call("tsdf_dense_reset", self._h)
 
-    def extract_mesh(self, normals=True, colors=True, faces=True):
+    def extract_mesh(self, normals=True, colors=True, faces=True, halo=None, global_x=None, keys=False):
         """Marching cubes at level 0 on the device (tsdf_dense_extract_mesh): (verts (N,3) f32
-        world, normals (N,3) f32, colors (N,3) u8, faces (M,3) i32); a field not asked for is None."""
+        world, normals (N,3) f32, colors (N,3) u8, faces (M,3) i32[, keys (N,) int64]); a field not
+        asked for is None.  A shard of a multi-GPU volume passes its neighbours' border rows:
+        halo = (global x (n,), tsdf (n,Y,Z), colour (n,Y,Z)) as numpy arrays or CUDA tensors
+        (sharding.mesh_shard does the exchange), global_x = the unsharded x extent."""
         nv, nt = ctypes.c_int64(), ctypes.c_int64()
-        _ffi.call("tsdf_dense_extract_mesh", self._h, ctypes.byref(nv), ctypes.byref(nt))
+        if halo is None and global_x is None:
+            _ffi.call("tsdf_dense_extract_mesh", self._h, ctypes.byref(nv), ctypes.byref(nt))
+        else:
+            gx, ht, hc = halo if halo is not None else (np.zeros(0, np.int64), None, None)
+            gx = np.ascontiguousarray(np.asarray(gx, dtype=np.int64))
+            dev = ht is not None and not isinstance(ht, np.ndarray)
+            if dev:
+                hp, cp = ht.data_ptr(), hc.data_ptr()
+            else:
+                ht = None if ht is None else np.ascontiguousarray(ht, dtype=np.float32)
+                hc = None if hc is None else np.ascontiguousarray(hc, dtype=np.float32)
+                hp, cp = _ffi.ptr(ht), _ffi.ptr(hc)
+            _ffi.call("tsdf_dense_extract_mesh_halo", self._h, int(global_x or self._vol_dim[0]), _ffi.ptr(gx),
+                      len(gx), hp, cp, _ffi.DEVICE_PTRS if dev else 0, ctypes.byref(nv), ctypes.byref(nt))
         v = np.empty((nv.value, 3), np.float32)
         n = np.empty((nv.value, 3), np.float32) if normals else None
         c = np.empty((nv.value, 3), np.uint8) if colors else None
         f = np.empty((nt.value, 3), np.int32) if faces else None
         _ffi.call("tsdf_dense_get_mesh", self._h, _ffi.ptr(v), _ffi.ptr(n), _ffi.ptr(c), _ffi.ptr(f))
-        return v, n, c, f
+        if not keys:
+            return v, n, c, f
+        k = np.empty(nv.value, np.int64)
+        _ffi.call("tsdf_dense_get_mesh_keys", self._h, _ffi.ptr(k))
+        return v, n, c, f, k
+
+    def mesh_halo_rows(self, global_x=None):
+        """Global x rows this shard's marching cubes reads but does not own (sorted)."""
+        gx = int(global_x or self._vol_dim[0])
+        n = ctypes.c_int64(0)
+        _ffi.call("tsdf_dense_mesh_halo_rows", self._h, gx, None, ctypes.byref(n))
+        rows = np.empty(n.value, np.int64)
+        _ffi.call("tsdf_dense_mesh_halo_rows", self._h, gx, _ffi.ptr(rows), ctypes.byref(n))
+        return rows
+
+    def get_rows(self, local_rows, weight=True, out=None):
+        """Local x rows in C-order (n, Y, Z): numpy (tsdf, weight, colour), or, with out = three
+        CUDA tensors (or None entries), filled on the device (no host copy)."""
+        rows = np.ascontiguousarray(np.asarray(local_rows, dtype=np.int64).reshape(-1))
+        if out is not None:
+            ptrs = [0 if o is None else o.data_ptr() for o in out]
+            _ffi.call("tsdf_dense_get_rows", self._h, _ffi.ptr(rows), len(rows),
+                      *[p if p else None for p in ptrs], _ffi.DEVICE_PTRS)
+            return out
+        shape = (len(rows), int(self._local_dim[1]), int(self._local_dim[2]))
+        t, c = np.empty(shape, np.float32), np.empty(shape, np.float32)
+        w = np.empty(shape, np.float32) if weight else None
+        _ffi.call("tsdf_dense_get_rows", self._h, _ffi.ptr(rows), len(rows), _ffi.ptr(t), _ffi.ptr(w),
+                  _ffi.ptr(c), 0)
+        return t, w, c
 
     def get_point_cloud(self):
         """grid_fusion.py:322-338: (N, 6) float32 rows x, y, z, r, g, b of the mesh vertices."""

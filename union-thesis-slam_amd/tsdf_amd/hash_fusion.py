@@ -217,6 +217,44 @@ class HashTable:
         _ffi.call("tsdf_hash_resize", self._h, 2 * n)
         print("Resize finished.")
 
+    # ------------------------------------------------------------------ sparse block transfer
+    def export_blocks(self, device=None):
+        """Live blocks: (bxyz (n,3) int32, tsdf, weight, colour (n,512) float32 in brick-local order,
+        occ (n,8) uint64 entry words) as numpy arrays, or as CUDA tensors on `device`."""
+        n = ctypes.c_int64(0)
+        _ffi.call("tsdf_hash_export_blocks", self._h, None, None, None, None, None, ctypes.byref(n), 0)
+        nb = n.value
+        if device is not None:
+            import torch
+            out = (torch.empty((nb, 3), dtype=torch.int32, device=device),
+                   *(torch.empty((nb, 512), dtype=torch.float32, device=device) for _ in range(3)),
+                   torch.empty((nb, 8), dtype=torch.int64, device=device))
+            if nb:
+                _ffi.call("tsdf_hash_export_blocks", self._h, *[o.data_ptr() for o in out], ctypes.byref(n),
+                          _ffi.DEVICE_PTRS)
+            return out
+        out = (np.empty((nb, 3), np.int32), *(np.empty((nb, 512), np.float32) for _ in range(3)),
+               np.empty((nb, 8), np.uint64))
+        if nb:
+            _ffi.call("tsdf_hash_export_blocks", self._h, *[_ffi.ptr(o) for o in out], ctypes.byref(n), 0)
+        return out
+
+    def import_blocks(self, bxyz, tsdf, weight, color, occ=None):
+        """Insert / overwrite whole blocks (numpy arrays or CUDA tensors, as export_blocks)."""
+        dev = not isinstance(bxyz, np.ndarray)
+        n = int(bxyz.shape[0])
+        if n == 0:
+            return
+        if dev:
+            ptrs = [None if a is None else a.contiguous().data_ptr() for a in (bxyz, tsdf, weight, color, occ)]
+        else:
+            arrs = [np.ascontiguousarray(bxyz, np.int32)] + [
+                None if a is None else np.ascontiguousarray(a, np.float32) for a in (tsdf, weight, color)] + [
+                None if occ is None else np.ascontiguousarray(occ, np.uint64)]
+            ptrs = [_ffi.ptr(a) for a in arrs]
+        _ffi.call("tsdf_hash_import_blocks", self._h, ptrs[0], n, ptrs[1], ptrs[2], ptrs[3], ptrs[4],
+                  _ffi.DEVICE_PTRS if dev else 0)
+
     # ------------------------------------------------------------------ export
     def get_volume(self):
         """hash_fusion.py:442-463: dense (tsdf, colour) float32 arrays of vol_dim."""

@@ -11,8 +11,11 @@ coordinates, hash_fusion.py:182-190) falls in [r*n/N, (r+1)*n/N) of the n-slot t
 §8(e)).  Again every rank sees every frame and the block sets are disjoint; the dense export
 merges them.
 
-Collectives (torch.distributed: RCCL "nccl" on the GPU box, "gloo" in the CPU tests) appear only
-outside the integrate loop: gathering the slabs / merging the hash exports and summing counters.
+Collectives (torch.distributed: RCCL "nccl" on the GPU box with device tensors, "gloo" on host
+tensors in the CPU tests) appear only outside the integrate loop: the device-side gather of the
+rows for get_volume, the point-to-point exchange of border rows for sharded marching cubes (the
+"border-slab" step of BASELINE config[3]: halo copies are identical on both sides, so the
+"reduce" is a select), the sparse block merge of hash shards, and counter sums.
 """
 from __future__ import annotations
 
@@ -68,50 +71,226 @@ def hash_owner(bx, by, bz, capacity: int, n_shards: int, int_bits: int = 64):
     return (home * n_shards) // capacity
 
 
+def _device(group=None):
+    """Where collective buffers live: the rank's GPU under RCCL ("nccl"), host memory under gloo
+    (the CPU tests)."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _all_x_index(x_index, group=None):
+    """Every rank's global x rows (list indexed by rank)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, [int(v) for v in x_index], group=group)
+    return [np.asarray(o, dtype=np.int64) for o in out]
+
+
 def gather_slabs(local: np.ndarray, x_range, nx: int, group=None, dst: int = 0):
     """Assemble x-slabs of an (x, Y, Z) array on rank `dst` (None elsewhere)."""
     return gather_rows(local, np.arange(x_range[0], x_range[1], dtype=np.int64), nx, group, dst)
 
 
-def gather_rows(local: np.ndarray, x_index, nx: int, group=None, dst: int = 0):
+def gather_rows(local, x_index, nx: int, group=None, dst: int = 0):
     """Assemble the x rows of an (x, Y, Z) array, local row i being global row x_index[i]
-    (slabs or cyclic columns), on rank `dst` (None elsewhere)."""
+    (slabs or cyclic columns), on rank `dst` (None elsewhere).  `local` is a numpy array or a
+    tensor; the rows travel in the backend's memory (device tensors under RCCL)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    dev = _device(group)
     x_index = np.asarray(x_index, dtype=np.int64)
-    if len(x_index) != local.shape[0]:
+    t = local if isinstance(local, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(local))
+    t = t.to(dev)
+    if len(x_index) != t.shape[0]:
         raise ValueError("x_index length differs from the local x extent")
-    t = torch.from_numpy(np.ascontiguousarray(local)).reshape(-1)
-    rows = torch.full((nx,), -1, dtype=torch.int64)
-    rows[: len(x_index)] = torch.from_numpy(x_index)
-    n_rows = [torch.zeros(nx, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(n_rows, rows, group=group)
-    row = int(np.prod(local.shape[1:], dtype=np.int64))
-    n_max = max(int((r >= 0).sum()) for r in n_rows) * row
-    buf = torch.zeros(n_max, dtype=t.dtype)
-    buf[: t.numel()] = t
-    parts = [torch.zeros(n_max, dtype=t.dtype) for _ in range(world)]
+    rows_all = _all_x_index(x_index, group)
+    row = int(np.prod(t.shape[1:], dtype=np.int64))
+    n_max = max(len(r) for r in rows_all) * row
+    buf = torch.zeros(n_max, dtype=t.dtype, device=dev)
+    buf[: t.numel()] = t.reshape(-1)
+    parts = [torch.empty(n_max, dtype=t.dtype, device=dev) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     if rank != dst:
         return None
-    out = np.empty((nx,) + local.shape[1:], dtype=local.dtype)
     seen = np.zeros(nx, dtype=np.int64)
-    for r_idx, p in zip(n_rows, parts):
-        xi = r_idx.numpy()
-        xi = xi[xi >= 0]
-        out[xi] = p[: len(xi) * row].numpy().reshape((len(xi),) + local.shape[1:])
+    out = torch.empty((nx,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+    for xi, p in zip(rows_all, parts):
+        out[torch.from_numpy(xi).to(dev)] = p[: len(xi) * row].reshape((len(xi),) + tuple(t.shape[1:]))
         seen[xi] += 1
     if not (seen == 1).all():
         raise RuntimeError("x rows missing or owned twice across ranks")
-    return out
+    return out.cpu().numpy()
+
+
+def gather_volume(vol, group=None, dst: int = 0, weight: bool = True):
+    """get_volume of a sharded TSDFVolume (grid_fusion.py:316-320): every rank reads its rows
+    straight from its brick layout into device buffers (tsdf_dense_get_rows), RCCL all-gathers
+    them, rank `dst` scatters them into the (X, Y, Z) volume on its GPU and copies it to the host
+    once.  Returns (tsdf, weight, colour) numpy arrays on `dst`, None elsewhere."""
+    import torch
+    dev = _device(group)
+    n = len(vol.x_index)
+    shape = (n, int(vol._local_dim[1]), int(vol._local_dim[2]))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        bufs = [torch.empty(shape, dtype=torch.float32, device=dev) if (k != 1 or weight) else None for k in range(3)]
+        vol.get_rows(np.arange(n), out=bufs)
+    else:
+        t, w, c = vol.get_rows(np.arange(n), weight=weight)
+        bufs = [torch.from_numpy(t), None if w is None else torch.from_numpy(w), torch.from_numpy(c)]
+    X = int(vol._vol_dim[0])
+    out = [None if b is None else gather_rows(b, vol.x_index, X, group, dst) for b in bufs]
+    return tuple(out) if out[0] is not None else None
+
+
+def exchange_halo(vol, group=None):
+    """The border rows each shard's marching cubes needs from its neighbours
+    (tsdf_dense_mesh_halo_rows), exchanged point to point: every rank reads the rows the others
+    need from its brick layout into one buffer (tsdf_dense_get_rows) and the pairs trade them
+    with batched isend / irecv (device tensors over xGMI under RCCL).  Returns (global x (n,),
+    tsdf (n,Y,Z), colour (n,Y,Z)) in this rank's memory for TSDFVolume.extract_mesh(halo=...)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = _device(group)
+    X = int(vol._vol_dim[0])
+    Y, Z = int(vol._local_dim[1]), int(vol._local_dim[2])
+    need = vol.mesh_halo_rows(X)
+    owners = _all_x_index(vol.x_index, group)
+    owner_of = np.full(X, -1, np.int64)
+    for r, xi in enumerate(owners):
+        owner_of[xi] = r
+    needs = [None] * world
+    dist.all_gather_object(needs, [int(v) for v in need], group=group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    local_row = {int(g): i for i, g in enumerate(vol.x_index)}
+    ops, recv = [], {}
+    for p in range(world):
+        if p == rank:
+            continue
+        give = [g for g in needs[p] if owner_of[g] == rank]  # rows p needs from me
+        take = [g for g in need if owner_of[g] == p]          # rows I need from p
+        if give:
+            lr = np.array([local_row[g] for g in give], np.int64)
+            if dev.type == "cuda":
+                sb = torch.empty((2, len(lr), Y, Z), dtype=torch.float32, device=dev)
+                vol.get_rows(lr, out=[sb[0], None, sb[1]])
+            else:
+                t, _, c = vol.get_rows(lr, weight=False)
+                sb = torch.from_numpy(np.stack([t, c]))
+            ops.append(dist.P2POp(dist.isend, sb, p, group=group))
+        if take:
+            rb = torch.empty((2, len(take), Y, Z), dtype=torch.float32, device=dev)
+            recv[p] = (take, rb)
+            ops.append(dist.P2POp(dist.irecv, rb, p, group=group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    missing = [g for g in need if owner_of[g] < 0]
+    if missing:
+        raise RuntimeError(f"halo rows {missing[:4]} are owned by no rank")
+    gx = np.concatenate([np.asarray(recv[p][0], np.int64) for p in sorted(recv)]) if recv else np.zeros(0, np.int64)
+    if not recv:
+        return gx, None, None
+    order = np.argsort(gx, kind="stable")  # rows in increasing x
+    gx = gx[order]
+    sel = torch.from_numpy(order).to(dev)
+    ht = torch.cat([recv[p][1][0] for p in sorted(recv)])[sel]
+    hc = torch.cat([recv[p][1][1] for p in sorted(recv)])[sel]
+    if dev.type == "cpu":
+        ht, hc = ht.numpy(), hc.numpy()
+    else:
+        ht, hc = ht.contiguous(), hc.contiguous()
+    return gx, ht, hc
+
+
+def mesh_shard(vol, group=None):
+    """Marching cubes of one shard with its halo (exchange_halo): the cells anchored at the
+    shard's own rows, vertices carrying their global keys.  Returns (verts, faces, normals,
+    colors, keys) numpy arrays; merge_meshes unites the shards' meshes."""
+    gx, ht, hc = exchange_halo(vol, group)
+    v, n, c, f, k = vol.extract_mesh(halo=(gx, ht, hc) if ht is not None else None,
+                                     global_x=int(vol._vol_dim[0]), keys=True)
+    return v, f, n, c, k
+
+
+def merge_meshes(parts):
+    """Union of shard meshes (verts, faces, normals, colors, keys): vertices merged by global key
+    (the copies of a border vertex are bit-identical), ordered by key like the unsharded mesh's
+    (voxel, axis) C-order; faces re-indexed.  Returns (verts, faces, normals, colors)."""
+    keys = np.concatenate([p[4] for p in parts])
+    uk, first = np.unique(keys, return_index=True)
+    verts = np.concatenate([p[0] for p in parts])[first]
+    norms = np.concatenate([p[2] for p in parts])[first]
+    cols = np.concatenate([p[3] for p in parts])[first]
+    faces = [np.searchsorted(uk, p[4][p[1]]).astype(np.int32) for p in parts if len(p[1])]
+    faces = np.concatenate(faces) if faces else np.zeros((0, 3), np.int32)
+    return verts, faces, norms, cols
+
+
+def gather_meshes(part, group=None, dst: int = 0):
+    """All shards' meshes on rank `dst`, merged (merge_meshes); None elsewhere."""
+    import torch.distributed as dist
+    parts = [None] * dist.get_world_size(group) if dist.get_rank(group) == dst else None
+    dist.gather_object(part, parts, dst=dst, group=group)
+    return merge_meshes(parts) if parts is not None else None
+
+
+def merge_hash_shards(ht, make_table, group=None, dst: int = 0):
+    """Merge bucket-range hash shards (disjoint block sets) into one table on rank `dst`: each rank
+    exports only its live blocks (tsdf_hash_export_blocks, device buffers under RCCL), the blocks
+    are gathered to `dst` and imported into `make_table()` (an unsharded HashTable).  Ownership is
+    carried by the blocks themselves, so entries with weight 0 survive.  Returns the merged table
+    on `dst`, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = _device(group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        blocks = ht.export_blocks(device=dev)
+    else:
+        blocks = [torch.from_numpy(b.view(np.int64) if b.dtype == np.uint64 else b) for b in ht.export_blocks()]
+    cnt = torch.tensor([blocks[0].shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    n_max = max(counts)
+    merged = make_table() if rank == dst else None
+    fields = []
+    for b in blocks:  # one field at a time keeps the padded buffers small
+        pad = torch.zeros((n_max,) + tuple(b.shape[1:]), dtype=b.dtype, device=dev)
+        pad[: b.shape[0]] = b
+        got = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+        dist.gather(pad, got, dst=dst, group=group)
+        if rank == dst:
+            fields.append(torch.cat([g[:c] for g, c in zip(got, counts)]))
+    if rank != dst:
+        return None
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        merged.import_blocks(fields[0], fields[1], fields[2], fields[3], fields[4])
+    else:
+        arr = [f.numpy() for f in fields]
+        merged.import_blocks(arr[0], arr[1], arr[2], arr[3], arr[4].view(np.uint64))
+    return merged
 
 
 def merge_hash_exports(tsdf, weight, color, group=None):
     """Merge per-shard dense exports (disjoint voxel sets: a voxel is owned where its weight
-    is > 0) into the full volume on every rank."""
+    is > 0) into the full volume on every rank.  Dense and host-side: kept for small volumes;
+    merge_hash_shards moves only live blocks."""
     import torch
     import torch.distributed as dist
 
@@ -129,11 +308,11 @@ def merge_hash_exports(tsdf, weight, color, group=None):
 
 
 def sum_counters(d: dict, group=None) -> dict:
-    """All-reduce (sum) a dict of integer counters."""
+    """All-reduce (sum) a dict of integer counters (in the backend's memory)."""
     import torch
     import torch.distributed as dist
 
     keys = sorted(k for k, v in d.items() if isinstance(v, (int, np.integer)))
-    t = torch.tensor([int(d[k]) for k in keys], dtype=torch.int64)
+    t = torch.tensor([int(d[k]) for k in keys], dtype=torch.int64, device=_device(group))
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return {k: int(v) for k, v in zip(keys, t.tolist())}
