@@ -140,7 +140,7 @@ def test_config4_rank_hash_shard_1024_extent():
         m = found.reshape(-1)
         assert _same(t[m], T.reshape(-1)[m]) and _same(w[m], W.reshape(-1)[m]) and _same(c[m], C.reshape(-1)[m])
     info = ht.info()
-    assert info["used"] > 10_000 and ht.stats()["bricks_skipped"] == 0
+    assert info["used"] > 10_000 and ht.stats()["list_errors"] == 0
 
 
 def test_hash_f32_state_within_1e4_of_reference_f64_voxels_over_500_frames():
