@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-dropin", action="store_true", help="skip the per-frame integrate() measurement")
     ap.add_argument("--dropin-frames", type=int, default=256)
     ap.add_argument("--no-mesh", action="store_true", help="skip the mesh-extraction measurement")
+    ap.add_argument("--depth-f64", action="store_true",
+                    help="A/B: keep the resident depth as float64 metres (the f64-texel integrate)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: several ranks may share a GPU)")
     return ap.parse_args()
@@ -86,8 +88,10 @@ def frame_ranges(start, count, F):
 
 def run_timed(vol, depth, rgb, K, Tinv, start, count, F, sync, barrier, profile, async_=True):
     """Issue `count` frames (asynchronously unless async_=False); returns wall seconds."""
+    from tsdf_amd import _ffi
     dptr, cptr = depth.data_ptr(), rgb.data_ptr()
-    dstride, cstride = depth[0].numel() * 2, rgb[0].numel()
+    dstride, cstride = depth[0].numel() * depth.element_size(), rgb[0].numel()
+    dk = _ffi.DEPTH_F64_M if depth.element_size() == 8 else _ffi.DEPTH_U16_MM
     hw = tuple(depth.shape[1:3])
     vol.set_profiling(profile)
     vol.stats(reset=True)
@@ -96,7 +100,7 @@ def run_timed(vol, depth, rgb, K, Tinv, start, count, F, sync, barrier, profile,
     t0 = time.perf_counter()
     for s, n in frame_ranges(start, count, F):
         vol.integrate_batch(dptr + s * dstride, cptr + s * cstride, K, Tinv[s:s + n], hw=hw,
-                            device_ptrs=True, sync=not async_)
+                            device_ptrs=True, sync=not async_, depth_kind=dk)
     vol.sync()
     sync()
     return time.perf_counter() - t0
@@ -238,6 +242,8 @@ def main():
         rgb[s:s + len(c)] = c
     Tinv = np.ascontiguousarray(np.linalg.inv(poses))
     K = scene.intrinsics()
+    if args.depth_f64:  # NumPy's f64(u16) / 1000: the same metres the u16 path computes
+        depth = torch.from_numpy(depth.cpu().numpy().view(np.uint16).astype(np.float64) / 1000.0).to(dev)
     sync()
     log(f"[rank {rank}] generated {F} frames in HBM in {time.perf_counter() - t0:.1f}s")
 

@@ -29,7 +29,7 @@ def per_kernel(path, counter):
     return out
 
 
-def main(tag="r01"):
+def main(tag="r02"):
     src = os.path.join(REPO, "gpurun_out", "profile")
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -40,7 +40,9 @@ def main(tag="r01"):
         f.write(line)
     fetch = per_kernel(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
-    summary = {"note": __doc__.strip().splitlines()[-4:], "kernels": {}}
+    sys.path.insert(0, REPO)
+    import bench
+    summary = {"note": __doc__.strip().splitlines()[-4:], "kernels": {}, "workload": bench.WORKLOAD}
     for k in sorted(set(fetch) | set(write)):
         fk = statistics.median(fetch.get(k, [0.0])) * 1024.0
         wk = statistics.median(write.get(k, [0.0])) * 1024.0
