@@ -525,7 +525,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
         // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
         // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
-        double zc[NZ], uu[NZ], vv[NZ];
+        // the pixel indices leave the f64 domain at once (saturating v_cvt_i32_f64: out-of-range
+        // values clamp to INT_MIN / INT_MAX and fail the unsigned bounds test below), which keeps
+        // two f64 per step out of the registers live across the gathers (no VGPR spill left)
+        double zc[NZ];
+        int iu[NZ], iv[NZ];
         unsigned inb = 0, slow = 0;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
@@ -543,8 +547,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const bool ok = fabs(sx - ux) < fr.half_m && fabs(sy - uy) < fr.half_m;
             const bool in = col_in && k < nz && z > 0.0;
             zc[k] = z;
-            uu[k] = ux;
-            vv[k] = uy;
+            iu[k] = cvt_i32_sat(ux);
+            iv[k] = cvt_i32_sat(uy);
             inb |= (unsigned)in << k;
             slow |= (unsigned)(in && !ok) << k;
         }
@@ -555,8 +559,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
                 const double x = fr.T[3] + fma(fr.T[2], pz, a0);
                 const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-                uu[k] = rint((x * fr.fx) / zc[k] + fr.cx);  // the reference's own operation order
-                vv[k] = rint((y * fr.fy) / zc[k] + fr.cy);
+                iu[k] = cvt_i32_sat(rint((x * fr.fx) / zc[k] + fr.cx));  // the reference's own operation order
+                iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
             }
         }
         unsigned cand = 0;
@@ -564,13 +568,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         const int W = fr.W, H = fr.H;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            // saturating conversion, then unsigned bounds: out-of-range values clamp to INT_MIN /
-            // INT_MAX and fail.  uu, vv are integral and not NaN wherever z > 0: the exact path
-            // yields NaN only for a non-finite pose, whose z (np.linalg.inv: all NaN) fails z > 0
-            const int iu = cvt_i32_sat(uu[k]), iv = cvt_i32_sat(vv[k]);
-            const bool c = ((inb >> k) & 1u) && (unsigned)iu < (unsigned)W && (unsigned)iv < (unsigned)H;
+            // unsigned bounds on the saturated indices (they come from integral, non-NaN values
+            // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
+            // np.linalg.inv: all NaN -- fails z > 0)
+            const bool c = ((inb >> k) & 1u) && (unsigned)iu[k] < (unsigned)W && (unsigned)iv[k] < (unsigned)H;
             cand |= (unsigned)c << k;
-            pix[k] = c ? __umul24((unsigned)iv, (unsigned)W) + (unsigned)iu : 0u;  // v_mad_u32_u24
+            pix[k] = c ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
         }
         // phase 2: gather depth and colour for every step at once, before the depth test, so
         // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
