@@ -210,11 +210,15 @@ int check_frame_args(const void* depth, int dk, const void* color, int ck, int H
     return TSDF_OK;
 }
 
-// World-space half-spaces n.p + d >= 0 (unit n) that contain every voxel the reference can
-// update for this frame: z > 0 and -0.5 <= u < W - 0.5, -0.5 <= v < H - 0.5, each widened by
-// one pixel (grid_fusion.py:273-277).  Camera-space plane (a, b, c, e) maps to world space
-// through the rows of world_to_cam.
+// Half-spaces n.q + d >= 0 (unit n, q = world point - camera centre) that contain every voxel
+// the reference can update for this frame: z > 0 and -0.5 <= u < W - 0.5, -0.5 <= v < H - 0.5,
+// each widened by one pixel (grid_fusion.py:273-277).  Camera-space plane (a, b, c, e) maps to
+// world space through the rows of world_to_cam; relative to the camera centre its offset is
+// small whatever the volume's distance from the world origin, so the cull's f32 test is exact to
+// ~1e-6 m there too (a 1e-4 m slack covers it).
 static void frustum_planes(Frame* fr, const double* T, int W, int H) {
+    for (int a = 0; a < 3; ++a)  // camera centre: -R^T t of world_to_cam = [R | t]
+        fr->eye[a] = -(T[a] * T[3] + T[4 + a] * T[7] + T[8 + a] * T[11]);
     const double cam[5][4] = {{0.0, 0.0, 1.0, 1e-4},
                               {fr->fx, 0.0, fr->cx + 1.5, 0.0},
                               {-fr->fx, 0.0, (double)W + 0.5 - fr->cx, 0.0},
@@ -225,6 +229,7 @@ static void frustum_planes(Frame* fr, const double* T, int W, int H) {
         for (int a = 0; a < 3; ++a)
             n[a] = cam[i][0] * T[0 + a] + cam[i][1] * T[4 + a] + cam[i][2] * T[8 + a];
         d += cam[i][0] * T[3] + cam[i][1] * T[7] + cam[i][2] * T[11];
+        d += n[0] * fr->eye[0] + n[1] * fr->eye[1] + n[2] * fr->eye[2];  // relative to the eye
         const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
         const double s = len > 0.0 ? 1.0 / len : 0.0;
         for (int a = 0; a < 3; ++a) fr->planes[i][a] = (float)(n[a] * s);

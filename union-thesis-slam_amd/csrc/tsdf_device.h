@@ -57,7 +57,10 @@ struct Frame {
     const void* color;        // the caller's colour (RGB8 or folded f32)
     const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
-    float planes[5][4];       // world-space half-spaces containing every valid voxel (cull)
+    float planes[5][4];       // half-spaces n.q + d >= 0 containing every valid voxel, q = world
+                              // point - eye (cull; camera-relative, so f32 stays accurate for
+                              // volumes far from the world origin)
+    double eye[3];            // camera centre in world coordinates
 };
 
 // Layout of a frame's max-depth pyramid (levels 1..kPyrLevels concatenated), the same for every
@@ -190,14 +193,14 @@ __device__ inline double vox_world(float origin, double vs, int g) {
 struct BrickBox {
     double p0[3];  // world position of the low corner voxel (f64, exact lattice)
     float ext[3];  // (hi - lo) * vs per axis
-    float ctr[3];  // centre of the voxel-centre box
+    float ctr[3];  // centre of the voxel-centre box, relative to the frame's camera centre
     float rad;     // its half diagonal + 0.1 mm
 };
 
 // Box of the voxel centres of bricks [b, b + n) per axis (n = 1: one brick; larger: a superbrick,
 // whose x extent spans the gaps between a cyclic shard's columns -- a superset, fine for culling).
-__device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz, int nx = 1, int ny = 1,
-                                     int nz = 1) {
+__device__ inline BrickBox brick_box(const Vol& v, const double* eye, int bx, int by, int bz, int nx = 1,
+                                     int ny = 1, int nz = 1) {
     const int bb[3] = {bx, by, bz}, nn[3] = {nx, ny, nz};
     BrickBox r;
 #pragma unroll
@@ -209,7 +212,7 @@ __device__ inline BrickBox brick_box(const Vol& v, int bx, int by, int bz, int n
         const int ghi = (a == 0) ? (hi >> 3) * v.xstride + (hi & 7) : hi;
         r.p0[a] = (double)v.origin[a] + v.vs * (double)(glo + v.off[a]);
         r.ext[a] = (float)(v.vs * (double)(ghi - glo));
-        r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(ghi - glo));
+        r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(ghi - glo) - eye[a]);
     }
     r.rad = 0.5f * sqrtf(r.ext[0] * r.ext[0] + r.ext[1] * r.ext[1] + r.ext[2] * r.ext[2]) + 1e-4f;
     return r;
@@ -803,13 +806,13 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
     const unsigned e = (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz);
     for (int f = f0; f < bt.n; f += kCullWG / 64) {  // wave w: frames w, w + 8
         const Frame& fr = bt.f[f];
-        if (cull_brick(v, fr, bt.pg, brick_box(v, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
+        if (cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
             bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
             if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership
                 const long long home = ref_hash(bx, by, bz, tab.shard_cap, tab.int_bits);
                 test = (int)((home * v.n_shards) / tab.shard_cap) == v.shard;
             }
-            if (test && cull_brick(v, fr, bt.pg, brick_box(v, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
+            if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
         }
     }
     __syncthreads();
