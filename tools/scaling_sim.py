@@ -4,7 +4,7 @@
 max over its ranks (ranks never exchange data while integrating).  Compares contiguous slabs
 with cyclic 8-voxel column shards.
 
-  python tools/scaling_sim.py [--steps 500] [--warmup 50] [--worlds 1,2,4,8]
+  python tools/scaling_sim.py [--steps 800] [--warmup 48] [--worlds 1,2,4,8]
 """
 import argparse
 import contextlib
@@ -21,8 +21,8 @@ sys.path.insert(0, os.path.join(REPO, "union-thesis-slam_amd"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=800, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--only", default=None, help="W:R -- time only rank R of world W (for profiling)")
@@ -31,8 +31,8 @@ def main():
     from tsdf_amd import grid_fusion, scene, sharding
     dev = torch.device("cuda", 0)
     F = a.frames
-    poses = scene.trajectory(F, seed=0)
-    sph = scene.make_spheres(0)
+    poses = scene.trajectory(F, seed=0, radius_frac=scene.BENCH_RING)  # the bench's workload
+    sph = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
     depth = torch.empty((F, 480, 640), dtype=torch.int16, device=dev)
     rgb = torch.empty((F, 480, 640, 3), dtype=torch.uint8, device=dev)
     for s in range(0, F, 50):

@@ -36,6 +36,9 @@ struct tsdf_hash {
     long long max_delta = 0;      // largest growth of live blocks between two reports
     long long tomb_est = 0;       // tombstones at the last table scan (only remove() adds them)
     bool async_pending = false;   // asynchronous launches since the last overflow check
+    // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
+    // 156-161); TSDF_HASH_MAX_LOAD overrides it for the load-factor sweep (tools/hash_sweep.py)
+    double max_load = 0.75;
 };
 
 namespace {
@@ -436,7 +439,7 @@ int ensure_room(tsdf_hash* h) {
     // the block pool keeps the same headroom as the table: live blocks below 0.75 of it
     if ((double)(h->host_st.pool_top - h->host_st.free_count + 64) >= 0.75 * (double)h->t.max_blocks)
         TSDF_TRY(grow_pool(h, h->t.max_blocks * 2));
-    if ((double)(inf.used + inf.tomb) >= 0.75 * (double)h->t.capacity)
+    if ((double)(inf.used + inf.tomb) >= h->max_load * (double)h->t.capacity)
         TSDF_TRY(resize_table(h, h->t.capacity * 2));
     return TSDF_OK;
 }
@@ -495,7 +498,7 @@ int async_room(tsdf_hash* h, long long s) {
     const long long step = std::max<long long>({h->max_delta, h->t.max_blocks / 12, 64});
     const long long need = used + 3 * step;
     if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, 2 * need)));
-    while ((double)(used + 3 * std::max<long long>(h->max_delta, 64) + h->tomb_est) >= 0.75 * (double)h->t.capacity)
+    while ((double)(used + 3 * std::max<long long>(h->max_delta, 64) + h->tomb_est) >= h->max_load * (double)h->t.capacity)
         TSDF_TRY(resize_table(h, h->t.capacity * 2));
     return TSDF_OK;
 }
@@ -712,7 +715,7 @@ int insert_block_keys(tsdf_hash* h, const std::vector<unsigned long long>& keys,
     TSDF_TRY(read_state(h));
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
-    while ((double)(inf.used + inf.tomb + nk) >= 0.75 * (double)h->t.capacity) {
+    while ((double)(inf.used + inf.tomb + nk) >= h->max_load * (double)h->t.capacity) {
         TSDF_TRY(resize_table(h, h->t.capacity * 2));
         TSDF_TRY(info_raw(h, &inf));
     }
@@ -793,6 +796,10 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
                           hipGetErrorString(e));
     }
     if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;  // 0: in-line kernels
+    if (const char* e = getenv("TSDF_HASH_MAX_LOAD")) {
+        const double ml = atof(e);
+        if (ml > 0.0 && ml < 1.0) h->max_load = ml;
+    }
     if (r == TSDF_OK) r = tsdf_hash_reset(h);
     if (r != TSDF_OK) {
         std::string keep = tsdf_last_error();
