@@ -37,6 +37,17 @@ def main(out):
         _, depth, rgb, pose = load_lounge(f)
         vol.integrate(rgb, depth, K, pose)
         ht.integrate(rgb, depth, K, pose)
+    # the same frames ingested once on rank 0 and broadcast (sharding.integrate_broadcast)
+    with contextlib.redirect_stdout(io.StringIO()):
+        vb = grid_fusion.TSDFVolume(np.array(C1), 0.04, shard=(rank, world))
+    d = c = T = None
+    if rank == 0:
+        fr = [load_lounge(f) for f in range(3)]
+        d = np.stack([f[0] for f in fr]).astype(np.uint16)
+        c = np.stack([f[2] for f in fr])
+        T = np.linalg.inv(np.stack([f[3] for f in fr]))
+    sharding.integrate_broadcast(vb, K, d, c, T, chunk=2)
+    same_b = all(np.array_equal(a, b) for a, b in zip(vb.get_state(), vol.get_state()))
     part = sharding.mesh_shard(vol)
     mesh = sharding.gather_meshes(part)
     state = sharding.gather_volume(vol)
@@ -47,13 +58,13 @@ def main(out):
 
     merged = sharding.merge_hash_shards(ht, make_table)
     own_blocks = ht.info()["used"]
-    tot = sharding.sum_counters({"blocks": int(own_blocks)})
+    tot = sharding.sum_counters({"blocks": int(own_blocks), "bcast_ok": int(same_b)})
     if rank == 0:
         ht_t, ht_w, ht_c = merged.get_state()
         np.savez(os.path.join(out, "dist.npz"), v=mesh[0], f=mesh[1], n=mesh[2], c=mesh[3],
                  t=state[0], w=state[1], col=state[2], ht=ht_t, hw=ht_w, hc=ht_c,
                  merged_used=merged.info()["used"], shard_blocks=tot["blocks"],
-                 part_verts=len(part[0]))
+                 part_verts=len(part[0]), bcast_ok=tot["bcast_ok"])
     dist.barrier()
     dist.destroy_process_group()
 

@@ -123,6 +123,35 @@ def _halo_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _broadcast_worker(rank, world, port, out_dir):
+    """Rank 0 alone reads the lounge frames; every rank receives them by broadcast and integrates
+    its cyclic shard with the oracle; the gathered volume must be the unsharded one."""
+    import oracle as O
+    from tsdf_amd import sharding
+    dist = _init(rank, world, port)
+    nx = int(O.OracleTSDFVolume(np.array(C1), 0.04)._vol_dim[0])
+    xi = sharding.columns(rank, world, nx)
+    vol = O.OracleTSDFVolume(np.array(C1), 0.04, x_index=xi)
+    K = lounge_intrinsics()
+    d = c = T = None
+    if rank == 0:
+        fr = [load_lounge(f) for f in range(3)]
+        d = np.stack([f[0] for f in fr]).astype(np.uint16)
+        c = np.stack([f[2] for f in fr])
+        T = np.linalg.inv(np.stack([f[3] for f in fr]))
+    got = 0
+    for dd, cc, tt in sharding.broadcast_frames(d, c, T, chunk=2):
+        for i in range(len(dd)):
+            m = dd[i].astype(float) / 1000.0
+            m[m == 65.535] = 0
+            vol.integrate(cc[i], m, K, np.linalg.inv(tt[i]))
+            got += 1
+    full = [sharding.gather_rows(a, xi, nx) for a in (vol._tsdf_vol_cpu, vol._weight_vol_cpu, vol._color_vol_cpu)]
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "bcast.npz"), t=full[0], w=full[1], c=full[2], got=got)
+    dist.destroy_process_group()
+
+
 def _cyclic_worker(rank, world, port, out_dir):
     _dense_worker(rank, world, port, out_dir, cyclic=True)
 
@@ -223,3 +252,20 @@ def test_merge_meshes_unites_by_key():
     mv, mf, mn, mc = sharding.merge_meshes([a, b])
     assert np.array_equal(mv, v[[3, 0, 1, 2, 4]])  # keys 5, 10, 20, 30, 40
     assert np.array_equal(mf, np.array([[1, 2, 3], [3, 4, 0]]))
+
+
+def test_frames_ingested_once_and_broadcast_gloo(tmp_path):
+    """SURVEY §8(e) frame distribution: one rank ingests the host frames, the others receive them
+    by broadcast in chunks (sharding.broadcast_frames); each rank's shard then equals the same
+    rows of the unsharded volume."""
+    import oracle as O
+    _run(_broadcast_worker, tmp_path)
+    g = np.load(os.path.join(tmp_path, "bcast.npz"))
+    ref = O.OracleTSDFVolume(np.array(C1), 0.04)
+    K = lounge_intrinsics()
+    for f in range(3):
+        _, depth, rgb, pose = load_lounge(f)
+        ref.integrate(rgb, depth, K, pose)
+    assert int(g["got"]) == 3
+    assert np.array_equal(g["t"].view(np.uint32), ref._tsdf_vol_cpu.view(np.uint32))
+    assert np.array_equal(g["w"], ref._weight_vol_cpu) and np.array_equal(g["c"], ref._color_vol_cpu)

@@ -152,3 +152,4 @@ def test_two_rank_job_exchange_gather_and_hash_merge(tmp_path):
     for a, b in zip((g["ht"], g["hw"], g["hc"]), hfull.get_state()):
         assert np.array_equal(a, b)
     assert int(g["merged_used"]) == int(g["shard_blocks"]) == hfull.info()["used"]
+    assert int(g["bcast_ok"]) == 2  # both ranks: broadcast-fed shard == host-fed shard

@@ -316,3 +316,72 @@ def sum_counters(d: dict, group=None) -> dict:
     t = torch.tensor([int(d[k]) for k in keys], dtype=torch.int64, device=_device(group))
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return {k: int(v) for k, v in zip(keys, t.tolist())}
+
+
+def broadcast_frames(depth, rgb, Tinv, group=None, src: int = 0, chunk: int = 64):
+    """Frames ingested ONCE (on rank `src`, from host memory) and broadcast to every rank over
+    the backend (RCCL over xGMI: the PCIe link of one GPU carries each frame once; gloo on the
+    host in the CPU tests) -- SURVEY §8(e)'s frame distribution for the demo loop
+    grid_demo1.py:76-87.  Rank `src` passes (F,H,W) u16 depth, (F,H,W,3) u8 colour and (F,4,4)
+    world_to_cam; the others pass None.  Yields (depth, colour, world_to_cam) chunks of up to
+    `chunk` frames on every rank: device tensors under RCCL, numpy arrays under gloo.  A yielded
+    device chunk stays valid until the one after next is requested (two buffers)."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    dev = _device(group)
+    meta = [None]
+    if rank == src:
+        depth = np.ascontiguousarray(depth)
+        rgb = np.ascontiguousarray(rgb)
+        meta = [(tuple(depth.shape), str(depth.dtype), tuple(rgb.shape), np.ascontiguousarray(Tinv, np.float64))]
+    dist.broadcast_object_list(meta, src=src, group=group)
+    dshape, ddtype, cshape, T = meta[0]
+    F = dshape[0]
+    ddt = {"uint16": torch.int16, "int16": torch.int16, "float64": torch.float64}[ddtype]
+    bufs = []
+    for k, f0 in enumerate(range(0, F, chunk)):
+        n = min(chunk, F - f0)
+        if len(bufs) < 2:
+            bufs.append((torch.empty((chunk,) + dshape[1:], dtype=ddt, device=dev),
+                         torch.empty((chunk,) + cshape[1:], dtype=torch.uint8, device=dev)))
+        bd, bc = bufs[k % 2]
+        d, c = bd[:n], bc[:n]
+        if rank == src:
+            hd = torch.from_numpy(depth[f0:f0 + n].view(np.int16) if ddtype != "float64" else depth[f0:f0 + n])
+            hc = torch.from_numpy(rgb[f0:f0 + n])
+            if dev.type == "cuda":
+                hd, hc = hd.pin_memory(), hc.pin_memory()
+            d.copy_(hd, non_blocking=True)
+            c.copy_(hc, non_blocking=True)
+        # as bytes: neither RCCL nor gloo reduces int16, and a broadcast only moves bytes
+        dist.broadcast(d.view(torch.uint8), src=src, group=group)
+        dist.broadcast(c, src=src, group=group)
+        if dev.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+            yield d, c, T[f0:f0 + n]
+        else:
+            dn = d.numpy().view(np.uint16) if ddtype != "float64" else d.numpy()
+            yield dn, c.numpy(), T[f0:f0 + n]
+
+
+def integrate_broadcast(vol, K, depth=None, rgb=None, Tinv=None, group=None, src: int = 0, chunk: int = 64):
+    """Integrate host frames held by rank `src` into every rank's shard: each chunk is broadcast
+    (broadcast_frames) and integrated asynchronously from device memory while the next chunk
+    travels; returns after this rank's shard holds every frame."""
+    import torch.distributed as dist
+    dev = _device(group)
+    hw = None
+    for k, (d, c, T) in enumerate(broadcast_frames(depth, rgb, Tinv, group, src, chunk)):
+        if dev.type == "cuda":
+            if k >= 2:
+                vol.sync()  # the buffer the next chunk lands in was read by chunk k - 2
+            hw = tuple(d.shape[1:3])
+            from . import _ffi
+            dk = _ffi.DEPTH_F64_M if d.element_size() == 8 else _ffi.DEPTH_U16_MM
+            vol.integrate_batch(d.data_ptr(), c.data_ptr(), K, T, hw=hw, device_ptrs=True, sync=False,
+                                depth_kind=dk)
+        else:
+            vol.integrate_batch(d, c, K, T, sync=False)
+    vol.sync()
+    dist.barrier(group=group)
