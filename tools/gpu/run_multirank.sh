@@ -5,6 +5,6 @@ set -o pipefail
 mkdir -p gpurun_out/mr
 for n in 2 4; do
   timeout -k 10 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port $((29500 + n)) bench.py --gpus $n --steps 400 --warmup 40 --dist-backend gloo --no-ingest \
+    --master-port $((29500 + n)) bench.py --gpus $n --steps 50 --warmup 5 --dist-backend gloo --no-cpu \
     > gpurun_out/mr/n$n.json 2> gpurun_out/mr/n$n.err || exit $?
 done
