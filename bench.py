@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--no-dropin", action="store_true", help="skip the per-frame integrate() measurement")
     ap.add_argument("--dropin-frames", type=int, default=256)
     ap.add_argument("--no-mesh", action="store_true", help="skip the mesh-extraction measurement")
+    ap.add_argument("--no-lounge", action="store_true", help="skip the real-lounge 2 cm realism check")
     ap.add_argument("--depth-f64", action="store_true",
                     help="A/B: keep the resident depth as float64 metres (the f64-texel integrate)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -443,6 +444,45 @@ def main():
         del d64, ch
         torch.cuda.empty_cache()
 
+    # ---- realism check: the real lounge frames at 2 cm ------------------
+    lounge = None
+    if not args.no_lounge and n == 1:
+        from PIL import Image
+        root = os.path.join(REPO, "tests", "golden", "lounge")
+        nl = 10  # the depth frames committed with the tests (frames 0-9; colour for 0-2)
+        ld = np.stack([np.array(Image.open(os.path.join(root, "frame-%06d.depth.png" % i))) for i in range(nl)])
+        lc = np.zeros(ld.shape + (3,), np.uint8)
+        for i in range(3):
+            lc[i] = np.array(Image.open(os.path.join(root, "frame-%06d.color.jpg" % i)).convert("RGB"))
+        lp = np.stack([np.loadtxt(os.path.join(root, "frame-%06d.pose.txt" % i)) for i in range(nl)])
+        lK = np.loadtxt(os.path.join(root, "camera-intrinsics.txt"), delimiter=" ")
+        reps = 40  # the 10 frames cycled: 400 frames
+        dd = torch.from_numpy(np.ascontiguousarray(np.tile(ld, (reps, 1, 1)).astype(np.uint16).view(np.int16))).to(dev)
+        cc = torch.from_numpy(np.ascontiguousarray(np.tile(lc, (reps, 1, 1, 1)))).to(dev)
+        lT = np.ascontiguousarray(np.tile(np.linalg.inv(lp), (reps, 1, 1)))
+        lb = np.array([[-4.22106438, 3.86798203], [-2.6663104, 2.60146141], [0., 5.76272371]])  # hash_map_test.py:11
+        with contextlib.redirect_stdout(sys.stderr):
+            lv = grid_fusion.TSDFVolume(lb, VOXEL, device=gpu)
+        lv.integrate_batch(dd.data_ptr(), cc.data_ptr(), lK, lT[:40], hw=(480, 640), device_ptrs=True,
+                           invalid_65535=True)
+        lv.stats(reset=True)
+        sync()
+        t0 = time.perf_counter()
+        lv.integrate_batch(dd.data_ptr(), cc.data_ptr(), lK, lT, hw=(480, 640), device_ptrs=True, sync=False,
+                           invalid_65535=True)
+        lv.sync()
+        tl = time.perf_counter() - t0
+        ls = lv.stats()
+        lounge = {"frames_per_s": round(len(lT) / tl, 1), "frames": len(lT),
+                  "mvox_updates_per_s": round(ls["voxel_updates"] / tl / 1e6, 1),
+                  "mean_voxels_updated_per_frame": round(ls["voxel_updates"] / len(lT)),
+                  "volume": "405x264x289 @ 0.02 m (lounge bounds, hash_map_test.py:11)",
+                  "source": "tests/golden/lounge frames 0-9 (u16 PNG depth, 65535 masked on the device), "
+                            "cycled 40 times from HBM"}
+        log(f"[rank 0] lounge 2 cm: {len(lT) / tl:.0f} frames/s, V_f {ls['voxel_updates'] / len(lT):.0f}")
+        lv.close()
+        del dd, cc
+
     # ---- CPU baseline: the NumPy restatement of the reference CPU path --------------------
     cpu = None
     if rank == 0 and n == 1 and not args.no_cpu:
@@ -469,6 +509,7 @@ def main():
             "pcie_inclusive": ingest,
             "broadcast_ingest": bcast,
             "dropin": dropin,
+            "lounge_2cm": lounge,
             "mesh": mesh,
             "roofline": roof,
             "cpu_baseline": cpu,
