@@ -114,6 +114,7 @@ struct PoolState {
     long long free_count;  // blocks on the free list
     long long cursor;      // allocations made by the current launch
     long long n_overflow;  // bricks skipped for lack of space (re-run after growing)
+    long long tombs;       // keys tombstoned since the table was last rebuilt (>= tombstones in it)
 };
 
 // Pool state after launch `seq`, written by the committing thread into page-locked host memory

@@ -34,7 +34,7 @@ struct tsdf_hash {
     long long seq = 0;            // allocating launches issued so far
     long long rb_used = -1;       // live blocks in the last report read
     long long max_delta = 0;      // largest growth of live blocks between two reports
-    long long tomb_est = 0;       // tombstones at the last table scan (only remove() adds them)
+    long long tomb_est = 0;       // PoolState::tombs at the last read (only remove() adds tombstones)
     bool async_pending = false;   // asynchronous launches since the last overflow check
     // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
     // 156-161); TSDF_HASH_MAX_LOAD overrides it for the load-factor sweep (tools/hash_sweep.py)
@@ -200,6 +200,7 @@ __global__ void k_free_empty(Table t, const unsigned long long* keys, long long 
     for (int k = 0; k < 8; ++k)
         if (coh_load(&t.occ[blk * 8 + k])) return;
     coh_store(&t.keys[s], kTomb);
+    atomicAdd((unsigned long long*)&t.st->tombs, 1ull);
     const unsigned long long f = atomicAdd((unsigned long long*)&t.st->free_count, 1ull);
     coh_store(&t.free_list[f], (int)blk);
 }
@@ -353,6 +354,7 @@ int dev_alloc(DevBufs& bufs, T** out, size_t bytes) {
 int read_state(tsdf_hash* h) {
     TSDF_HIP(hipMemcpyAsync(&h->host_st, h->t.st, sizeof(PoolState), hipMemcpyDeviceToHost, h->b.stream));
     TSDF_HIP(hipStreamSynchronize(h->b.stream));
+    h->tomb_est = h->host_st.tombs;
     return TSDF_OK;
 }
 
@@ -405,8 +407,10 @@ int resize_table(tsdf_hash* h, long long new_cap) {
     TSDF_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_rehash, dim3(2048), dim3(256), 0, B.stream, h->t, nt);
     TSDF_HIP(hipGetLastError());
+    TSDF_HIP(hipMemsetAsync(&h->t.st->tombs, 0, sizeof(long long), B.stream));  // a rebuilt table has none
     TSDF_HIP(hipStreamSynchronize(B.stream));
     fresh.keep();
+    h->tomb_est = 0;
     (void)hipFree(h->t.keys);
     (void)hipFree(h->t.vals);
     h->t.keys = nt.keys;
@@ -431,15 +435,14 @@ int info_raw(tsdf_hash* h, InfoDev* out) {
 
 // Grow whatever ran out (reference policy: keep slots used below 0.75 of capacity, like
 // needs_resize, hash_fusion.py:156-161), then re-run the bricks that were skipped.
-int ensure_room(tsdf_hash* h) {
-    InfoDev inf{};
-    TSDF_TRY(info_raw(h, &inf));
-    h->tomb_est = (long long)inf.tomb;
-    TSDF_TRY(read_state(h));
+// Live keys = blocks handed out and not freed; tombstones are bounded by PoolState::tombs -- no
+// table scan per batch (k_info over 2^22 slots cost 1.5 ms).
+int ensure_room(tsdf_hash* h, bool fresh = false) {
+    if (!fresh) TSDF_TRY(read_state(h));  // fresh: host_st was read after the stream's last launch
+    const long long live = h->host_st.pool_top - h->host_st.free_count;
     // the block pool keeps the same headroom as the table: live blocks below 0.75 of it
-    if ((double)(h->host_st.pool_top - h->host_st.free_count + 64) >= 0.75 * (double)h->t.max_blocks)
-        TSDF_TRY(grow_pool(h, h->t.max_blocks * 2));
-    if ((double)(inf.used + inf.tomb) >= h->max_load * (double)h->t.capacity)
+    if ((double)(live + 64) >= 0.75 * (double)h->t.max_blocks) TSDF_TRY(grow_pool(h, h->t.max_blocks * 2));
+    if ((double)(live + h->host_st.tombs) >= h->max_load * (double)h->t.capacity)
         TSDF_TRY(resize_table(h, h->t.capacity * 2));
     return TSDF_OK;
 }
@@ -621,7 +624,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         if (sync) {
             TSDF_TRY(hash_after_batch(h, bi, dk, TSDF_COLOR_RGB8));
             TSDF_TRY(B.end_batch(flags, L % kSlots));
-            TSDF_TRY(ensure_room(h));
+            TSDF_TRY(ensure_room(h, true));
         } else {
             TSDF_TRY(B.end_batch(flags, L % kSlots));
         }
@@ -677,7 +680,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         }
         TSDF_TRY(hash_after_batch(h, bt, dk, ck));
         TSDF_TRY(B.end_batch(flags, slot));  // the overflow re-runs above read this batch's frames
-        TSDF_TRY(ensure_room(h));
+        TSDF_TRY(ensure_room(h, true));
     }
     TSDF_TRY(guard.finish());
     if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
