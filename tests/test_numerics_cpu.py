@@ -6,14 +6,15 @@ from conftest import REPO
 
 
 def test_depth_mm_to_metres_conversion_is_exact_for_every_u16(tmp_path):
-    """The kernels convert u16 millimetres with m*0.001 + one FMA correction instead of a
-    division; it must equal NumPy's astype(float)/1000. for all 65536 inputs."""
+    """The kernels convert u16 millimetres with a two-term 1/1000, fma(m, C_HI, m*C_LO), instead
+    of a division; it must equal NumPy's astype(float)/1000. for all 65536 inputs."""
     exe = os.path.join(tmp_path, "chk")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(REPO, "tools", "check_depth_conversion.c"),
                     "-o", exe, "-lm"], check=True)
     out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
-    assert "one-correction mismatches 0" in out, out
-    assert "mul-only mismatches 0" not in out  # the plain product alone would NOT be exact
+    assert "C_LO == RN(1/1000 - C_HI)" in out, out
+    assert "two-term mismatches 0," in out, out
+    assert "mul-only mismatches 0," not in out  # the plain product alone would NOT be exact
 
 
 def test_frustum_planes_contain_the_valid_pixel_range():

@@ -364,13 +364,11 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 
 
 // Depth in metres at pixel p exactly as NumPy computes it: u16 mm -> astype(float) / 1000.
-// (grid_demo1.py:81-82).  For u16 input the quotient is m * 0.001 with one FMA correction
-// (r = m - 1000 q exactly; q + r * 0.001), which equals RN(m / 1000) for every m in [0, 65535]
-// (checked exhaustively: tools/check_depth_conversion.c).
-// Depth of pixel p in metres = f64(u16) / 1000 (grid_fusion.py via the wrapper's encoding),
-// computed as q = m * 0.001 plus one FMA correction (exact for all 65536 inputs:
-// tools/check_depth_conversion.c).  depth_raw issues the u16 load; depth_m converts.  For f64
-// depth (DK == 1) depth_raw is unused and depth_m loads.
+// (grid_demo1.py:81-82).  For u16 input the quotient is fma(m, C_HI, m * C_LO) with the two-term
+// 1/1000 = C_HI + C_LO, which equals RN(m / 1000) for every m in [0, 65535] (checked
+// exhaustively: tools/check_depth_conversion.c) -- one f64 multiply fewer than q = m * 0.001 plus
+// an FMA correction.  depth_raw issues the u16 load; depth_m converts.  For f64 depth (DK == 1)
+// depth_raw is unused and depth_m loads.
 // p is a pixel index < 2^28 (check_frame_args), so byte offsets fit 32 bits: the loads take
 // the SGPR-base + 32-bit VGPR-offset form (no 64-bit address arithmetic per gather)
 template <typename T>
@@ -383,10 +381,9 @@ __device__ inline unsigned depth_raw(const Frame& fr, unsigned p) {
 }
 template <int DK>
 __device__ inline double depth_m(const Frame& fr, unsigned p, unsigned raw) {
-    if (DK == 0) {
+    if (DK == 0) {  // two-term 1/1000 = C_HI + C_LO: exact for every u16 (tools/check_depth_conversion.c)
         const double m = (double)raw;
-        const double q = m * 0.001;
-        return fma(fma(-q, 1000.0, m), 0.001, q);
+        return fma(m, 0.001, m * -2.0858186326137145e-20);
     }
     return texel<double>(fr.depth, p);
 }
