@@ -95,13 +95,16 @@ def test_async_hash_overflow_is_reported_not_replayed():
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("pipe", ["1", "0"])
-def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe):
+@pytest.mark.parametrize("pipe,vmm", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe, vmm):
     """Asynchronous hash calls read each launch's pool report two launches later and grow the
     pool / table before they fill: a continuing trajectory needs several growths and none of its
-    bricks is skipped; the result equals the dense grid."""
+    bricks is skipped; the result equals the dense grid.  The pool grows by mapping memory behind
+    its reserved address ranges (vmm = 1, launches in flight keep running) or, with
+    TSDF_HASH_VMM=0, by a drained copy into larger allocations."""
     from tsdf_amd import grid_fusion, hash_fusion
     monkeypatch.setenv("TSDF_PIPELINE", pipe)
+    monkeypatch.setenv("TSDF_HASH_VMM", vmm)
     d, c, poses = _synth(72, start=100)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     Tinv = np.linalg.inv(poses)

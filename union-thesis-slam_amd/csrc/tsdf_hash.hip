@@ -18,6 +18,74 @@
 
 using namespace tsdf;
 
+// A growable device array on the virtual-memory API: the address range for the largest size
+// is reserved at create and physical chunks are mapped behind it as the pool grows.  Growth
+// copies nothing and moves nothing, so launches already in flight (which only address blocks
+// below their own max_blocks) keep running while it happens.  Falls back to hipMalloc + copy
+// (grow_pool) when the reservation is refused.
+struct VArray {
+    char* base = nullptr;
+    size_t reserved = 0, mapped = 0, gran = 0;
+    int device = 0;
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
+    hipMemAllocationProp prop() const {
+        hipMemAllocationProp p{};
+        p.type = hipMemAllocationTypePinned;
+        p.location.type = hipMemLocationTypeDevice;
+        p.location.id = device;
+        return p;
+    }
+    bool reserve(int dev, size_t max_bytes) {  // false: VMM unavailable (use hipMalloc)
+        device = dev;
+        const hipMemAllocationProp p = prop();
+        if (hipMemGetAllocationGranularity(&gran, &p, hipMemAllocationGranularityMinimum) != hipSuccess || !gran)
+            return false;
+        reserved = (max_bytes + gran - 1) / gran * gran;
+        void* b = nullptr;
+        if (hipMemAddressReserve(&b, reserved, 0, nullptr, 0) != hipSuccess) return false;
+        base = (char*)b;
+        return true;
+    }
+    int grow(size_t bytes) {  // map [mapped, round_up(bytes))
+        const size_t want = (bytes + gran - 1) / gran * gran;
+        if (want <= mapped) return TSDF_OK;
+        if (want > reserved) return set_error(TSDF_E_CAPACITY, "pool beyond its reservation");
+        const size_t sz = want - mapped;
+        const hipMemAllocationProp p = prop();
+        hipMemGenericAllocationHandle_t hdl;
+        TSDF_HIP(hipMemCreate(&hdl, sz, &p, 0));
+        hipError_t e = hipMemMap(base + mapped, sz, 0, hdl, 0);
+        if (e != hipSuccess) {
+            (void)hipMemRelease(hdl);
+            TSDF_HIP(e);
+        }
+        hipMemAccessDesc acc{};
+        acc.location = p.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(base + mapped, sz, &acc, 1);
+        if (e != hipSuccess) {
+            (void)hipMemUnmap(base + mapped, sz);
+            (void)hipMemRelease(hdl);
+            TSDF_HIP(e);
+        }
+        chunks.emplace_back(hdl, sz);
+        mapped = want;
+        return TSDF_OK;
+    }
+    void release() {
+        size_t off = mapped;
+        for (auto it = chunks.rbegin(); it != chunks.rend(); ++it) {
+            off -= it->second;
+            (void)hipMemUnmap(base + off, it->second);
+            (void)hipMemRelease(it->first);
+        }
+        chunks.clear();
+        if (base) (void)hipMemAddressFree(base, reserved);
+        base = nullptr;
+        mapped = reserved = 0;
+    }
+};
+
 struct tsdf_hash {
     Base b;
     Table t{};          // device view (pointers + capacity)
@@ -39,6 +107,15 @@ struct tsdf_hash {
     // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
     // 156-161); TSDF_HASH_MAX_LOAD overrides it for the load-factor sweep (tools/hash_sweep.py)
     double max_load = 0.75;
+    // block pool on reserved address ranges (tsdf, weight, colour, entry words, free list)
+    bool vmm = false;
+    VArray va[5];
+    int map_pool(long long n) {  // back blocks [0, n) of every pool array
+        const size_t per[5] = {sizeof(float) * kBrickVox, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
+                               sizeof(unsigned long long) * 8, sizeof(int)};
+        for (int k = 0; k < 5; ++k) TSDF_TRY(va[k].grow(per[k] * (size_t)n));
+        return TSDF_OK;
+    }
 };
 
 namespace {
@@ -364,6 +441,11 @@ int grow_pool(tsdf_hash* h, long long new_max) {
     // the volume has n_bricks bricks: a pool never needs more blocks than that
     new_max = std::min<long long>(new_max, B.n_bricks);
     if (new_max <= t.max_blocks) return TSDF_OK;
+    if (h->vmm) {  // map more physical memory behind the reserved ranges: no copy, no drain
+        TSDF_TRY(h->map_pool(new_max));
+        t.max_blocks = new_max;
+        return TSDF_OK;
+    }
     const size_t old_n = (size_t)t.max_blocks, nn = (size_t)new_max;
     float *nt, *nw, *nc;
     unsigned long long* no;
@@ -782,13 +864,37 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         t.overflow_cap = (int)std::min<long long>(h->b.n_bricks, 1ll << 30);
         hipError_t e = hipMalloc(&t.keys, sizeof(unsigned long long) * capacity);
         if (e == hipSuccess) e = hipMalloc(&t.vals, sizeof(int) * capacity);
-        if (e == hipSuccess) e = hipMalloc(&t.occ, sizeof(unsigned long long) * 8 * max_blocks);
-        if (e == hipSuccess) e = hipMalloc(&t.free_list, sizeof(int) * max_blocks);
         if (e == hipSuccess) e = hipMalloc(&t.overflow, sizeof(ListEntry) * (size_t)t.overflow_cap);
         if (e == hipSuccess) e = hipMalloc(&t.st, sizeof(PoolState));
-        if (e == hipSuccess) e = hipMalloc(&h->b.pool.tsdf, sizeof(float) * kBrickVox * max_blocks);
-        if (e == hipSuccess) e = hipMalloc(&h->b.pool.weight, sizeof(float) * kBrickVox * max_blocks);
-        if (e == hipSuccess) e = hipMalloc(&h->b.pool.color, sizeof(float) * kBrickVox * max_blocks);
+        // the pool: address ranges for every brick of the volume, backed as it grows
+        // (TSDF_HASH_VMM=0: plain allocations, grown by copy)
+        const char* ev = getenv("TSDF_HASH_VMM");
+        const size_t nb = (size_t)h->b.n_bricks;
+        h->vmm = e == hipSuccess && !(ev && atoi(ev) == 0) &&
+                 h->va[0].reserve(device, nb * kBrickVox * sizeof(float)) &&
+                 h->va[1].reserve(device, nb * kBrickVox * sizeof(float)) &&
+                 h->va[2].reserve(device, nb * kBrickVox * sizeof(float)) &&
+                 h->va[3].reserve(device, nb * 8 * sizeof(unsigned long long)) &&
+                 h->va[4].reserve(device, nb * sizeof(int));
+        if (h->vmm && h->map_pool(max_blocks) != TSDF_OK) {  // fall back to plain allocations
+            for (auto& v : h->va) v.release();
+            h->vmm = false;
+        }
+        if (!h->vmm)
+            for (auto& v : h->va) v.release();
+        if (h->vmm) {
+            h->b.pool.tsdf = (float*)h->va[0].base;
+            h->b.pool.weight = (float*)h->va[1].base;
+            h->b.pool.color = (float*)h->va[2].base;
+            t.occ = (unsigned long long*)h->va[3].base;
+            t.free_list = (int*)h->va[4].base;
+        } else {
+            if (e == hipSuccess) e = hipMalloc(&t.occ, sizeof(unsigned long long) * 8 * max_blocks);
+            if (e == hipSuccess) e = hipMalloc(&t.free_list, sizeof(int) * max_blocks);
+            if (e == hipSuccess) e = hipMalloc(&h->b.pool.tsdf, sizeof(float) * kBrickVox * max_blocks);
+            if (e == hipSuccess) e = hipMalloc(&h->b.pool.weight, sizeof(float) * kBrickVox * max_blocks);
+            if (e == hipSuccess) e = hipMalloc(&h->b.pool.color, sizeof(float) * kBrickVox * max_blocks);
+        }
         if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_rb, sizeof(PoolReport) * kReports, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) {
             std::memset(h->h_rb, 0, sizeof(PoolReport) * kReports);
@@ -818,10 +924,16 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
     if (!h) return TSDF_OK;
     (void)hipSetDevice(h->b.device);
     h->b.release();
-    void* ps[] = {h->t.keys, h->t.vals, h->t.occ, h->t.free_list, h->t.overflow, h->t.st,
-                  h->b.pool.tsdf, h->b.pool.weight, h->b.pool.color, h->d_list};
+    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list};
     for (void* p : ps)
         if (p) (void)hipFree(p);
+    if (h->vmm) {
+        for (auto& v : h->va) v.release();
+    } else {
+        void* pool[] = {h->t.occ, h->t.free_list, h->b.pool.tsdf, h->b.pool.weight, h->b.pool.color};
+        for (void* p : pool)
+            if (p) (void)hipFree(p);
+    }
     if (h->h_rb) (void)hipHostFree(h->h_rb);
     delete h;
     return TSDF_OK;
