@@ -38,11 +38,18 @@ struct VArray {
     bool reserve(int dev, size_t max_bytes) {  // false: VMM unavailable (use hipMalloc)
         device = dev;
         const hipMemAllocationProp p = prop();
-        if (hipMemGetAllocationGranularity(&gran, &p, hipMemAllocationGranularityMinimum) != hipSuccess || !gran)
+        // the recommended granularity (the physical page the mapping is made of): chunks mapped at
+        // offsets of the minimum granularity only were refused by hipMemMap
+        if (hipMemGetAllocationGranularity(&gran, &p, hipMemAllocationGranularityRecommended) != hipSuccess || !gran) {
+            (void)hipGetLastError();  // leave no sticky error behind
             return false;
+        }
         reserved = (max_bytes + gran - 1) / gran * gran;
         void* b = nullptr;
-        if (hipMemAddressReserve(&b, reserved, 0, nullptr, 0) != hipSuccess) return false;
+        if (hipMemAddressReserve(&b, reserved, gran, nullptr, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
         base = (char*)b;
         return true;
     }
@@ -53,20 +60,22 @@ struct VArray {
         const size_t sz = want - mapped;
         const hipMemAllocationProp p = prop();
         hipMemGenericAllocationHandle_t hdl;
-        TSDF_HIP(hipMemCreate(&hdl, sz, &p, 0));
-        hipError_t e = hipMemMap(base + mapped, sz, 0, hdl, 0);
-        if (e != hipSuccess) {
-            (void)hipMemRelease(hdl);
-            TSDF_HIP(e);
+        hipError_t e = hipMemCreate(&hdl, sz, &p, 0);
+        if (e == hipSuccess) {
+            e = hipMemMap(base + mapped, sz, 0, hdl, 0);
+            if (e == hipSuccess) {
+                hipMemAccessDesc acc{};
+                acc.location = p.location;
+                acc.flags = hipMemAccessFlagsProtReadWrite;
+                e = hipMemSetAccess(base + mapped, sz, &acc, 1);
+                if (e != hipSuccess) (void)hipMemUnmap(base + mapped, sz);
+            }
+            if (e != hipSuccess) (void)hipMemRelease(hdl);
         }
-        hipMemAccessDesc acc{};
-        acc.location = p.location;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        e = hipMemSetAccess(base + mapped, sz, &acc, 1);
         if (e != hipSuccess) {
-            (void)hipMemUnmap(base + mapped, sz);
-            (void)hipMemRelease(hdl);
-            TSDF_HIP(e);
+            (void)hipGetLastError();  // no sticky error: the caller falls back to plain allocations
+            return set_error(e == hipErrorOutOfMemory ? TSDF_E_OOM : TSDF_E_HIP, "pool mapping: %s",
+                             hipGetErrorString(e));
         }
         chunks.emplace_back(hdl, sz);
         mapped = want;
@@ -442,9 +451,11 @@ int grow_pool(tsdf_hash* h, long long new_max) {
     new_max = std::min<long long>(new_max, B.n_bricks);
     if (new_max <= t.max_blocks) return TSDF_OK;
     if (h->vmm) {  // map more physical memory behind the reserved ranges: no copy, no drain
-        TSDF_TRY(h->map_pool(new_max));
-        t.max_blocks = new_max;
-        return TSDF_OK;
+        if (h->map_pool(new_max) == TSDF_OK) {
+            t.max_blocks = new_max;
+            return TSDF_OK;
+        }
+        // mapping refused: continue with plain allocations (copy below, then unmap the ranges)
     }
     const size_t old_n = (size_t)t.max_blocks, nn = (size_t)new_max;
     float *nt, *nw, *nc;
@@ -464,11 +475,16 @@ int grow_pool(tsdf_hash* h, long long new_max) {
     TSDF_HIP(hipMemcpyAsync(nf, t.free_list, old_n * sizeof(int), hipMemcpyDeviceToDevice, B.stream));
     TSDF_HIP(hipStreamSynchronize(B.stream));
     fresh.keep();
-    (void)hipFree(B.pool.tsdf);
-    (void)hipFree(B.pool.weight);
-    (void)hipFree(B.pool.color);
-    (void)hipFree(t.occ);
-    (void)hipFree(t.free_list);
+    if (h->vmm) {
+        for (auto& v : h->va) v.release();
+        h->vmm = false;
+    } else {
+        (void)hipFree(B.pool.tsdf);
+        (void)hipFree(B.pool.weight);
+        (void)hipFree(B.pool.color);
+        (void)hipFree(t.occ);
+        (void)hipFree(t.free_list);
+    }
     B.pool.tsdf = nt;
     B.pool.weight = nw;
     B.pool.color = nc;
