@@ -318,14 +318,15 @@ def sum_counters(d: dict, group=None) -> dict:
     return {k: int(v) for k, v in zip(keys, t.tolist())}
 
 
-def broadcast_frames(depth, rgb, Tinv, group=None, src: int = 0, chunk: int = 64):
+def broadcast_frames(depth, rgb, Tinv, group=None, src: int = 0, chunk: int = 64, before_reuse=None):
     """Frames ingested ONCE (on rank `src`, from host memory) and broadcast to every rank over
     the backend (RCCL over xGMI: the PCIe link of one GPU carries each frame once; gloo on the
     host in the CPU tests) -- SURVEY §8(e)'s frame distribution for the demo loop
     grid_demo1.py:76-87.  Rank `src` passes (F,H,W) u16 depth, (F,H,W,3) u8 colour and (F,4,4)
     world_to_cam; the others pass None.  Yields (depth, colour, world_to_cam) chunks of up to
-    `chunk` frames on every rank: device tensors under RCCL, numpy arrays under gloo.  A yielded
-    device chunk stays valid until the one after next is requested (two buffers)."""
+    `chunk` frames on every rank: device tensors under RCCL, numpy arrays under gloo.  Device
+    chunks alternate between two buffers: before a buffer is overwritten, `before_reuse()` is
+    called so that the consumer can finish the work still reading it (chunk k - 2)."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
@@ -347,6 +348,8 @@ def broadcast_frames(depth, rgb, Tinv, group=None, src: int = 0, chunk: int = 64
                          torch.empty((chunk,) + cshape[1:], dtype=torch.uint8, device=dev)))
         bd, bc = bufs[k % 2]
         d, c = bd[:n], bc[:n]
+        if k >= 2 and before_reuse is not None:
+            before_reuse()  # chunk k - 2 read this buffer
         if rank == src:
             hd = torch.from_numpy(depth[f0:f0 + n].view(np.int16) if ddtype != "float64" else depth[f0:f0 + n])
             hc = torch.from_numpy(rgb[f0:f0 + n])
@@ -372,10 +375,8 @@ def integrate_broadcast(vol, K, depth=None, rgb=None, Tinv=None, group=None, src
     import torch.distributed as dist
     dev = _device(group)
     hw = None
-    for k, (d, c, T) in enumerate(broadcast_frames(depth, rgb, Tinv, group, src, chunk)):
+    for d, c, T in broadcast_frames(depth, rgb, Tinv, group, src, chunk, before_reuse=vol.sync):
         if dev.type == "cuda":
-            if k >= 2:
-                vol.sync()  # the buffer the next chunk lands in was read by chunk k - 2
             hw = tuple(d.shape[1:3])
             from . import _ffi
             dk = _ffi.DEPTH_F64_M if d.element_size() == 8 else _ffi.DEPTH_U16_MM
