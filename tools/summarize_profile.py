@@ -60,5 +60,36 @@ def main(tag="r02"):
     print(json.dumps(summary, indent=1))
 
 
+def sq(tag="r02"):
+    """gpurun_out/pmc_sq/pmc_sq.csv (tools/gpu/run_pmc_sq.sh) -> profiles/pmc_sq_<tag>.json: SQ
+    counters per launch of the dense integrate launch and its VALU-busy fraction."""
+    src = os.path.join(REPO, "gpurun_out", "pmc_sq", "pmc_sq.csv")
+    per = {}
+    kernel = None
+    for row in csv.DictReader(open(src)):
+        k = row["Kernel_Name"].split("(")[0].replace("void ", "")
+        if not k.startswith("tsdf::k_fused<true"):
+            continue
+        kernel = k
+        per.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    med = {c: statistics.median(v) for c, v in sorted(per.items())}
+    sys.path.insert(0, REPO)
+    import bench
+    out = {"kernel": kernel, "median_per_launch": med,
+           # SQ_* cycle counters count quad-cycles; 1024 SIMDs, GRBM_GUI_ACTIVE summed over 8 XCDs
+           "valu_busy_per_simd": round(med["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * med["GRBM_GUI_ACTIVE"] / 8), 3),
+           "valu_per_vmem": round(med["SQ_INSTS_VALU"] / med["SQ_INSTS_VMEM"], 1),
+           "workload": bench.WORKLOAD,
+           "note": "rocprofv3 --pmc pass (tools/gpu/run_pmc_sq.sh, 50 steps); SQ_* cycle counters in "
+                   "quad-cycles per MI355X_MICROARCH.md; busy = ACTIVE_INST_VALU x 4 / (1024 SIMDs x "
+                   "GRBM_GUI_ACTIVE / 8 XCDs)"}
+    with open(os.path.join(REPO, "profiles", f"pmc_sq_{tag}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    if len(sys.argv) > 1 and sys.argv[1] == "sq":
+        sq(*sys.argv[2:])
+    else:
+        main(*sys.argv[1:])
