@@ -314,13 +314,16 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
         long long s = pos + lane;
         if (s >= t.capacity) s -= t.capacity;
         if (s >= t.capacity) s %= t.capacity;
+        // the slot values load beside the keys (one memory latency per probe step instead of two);
+        // a key found here was inserted by an earlier launch or by this wave, so its value is set
         const unsigned long long kk = coh_load(&t.keys[s]);
+        const int vv = coh_load(&t.vals[s]);
         const unsigned long long hit = __ballot(kk == key);
         if (hit) {
             const int l = __ffsll((long long)hit) - 1;
             slot_out = __shfl(s, l);
             probe = scanned + l;
-            return coh_load(&t.vals[slot_out]);
+            return __shfl(vv, l);
         }
         const unsigned long long emp = __ballot(kk == kEmpty);
         unsigned long long tm = __ballot(kk == kTomb);
