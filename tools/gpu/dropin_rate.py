@@ -1,0 +1,43 @@
+"""Per-frame integrate() rate from host NumPy (the reference's call pattern), several passes, for
+A/B of the host copy path (TSDF_COPY_THREADS):  python tools/gpu/dropin_rate.py [frames] [passes]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from tsdf_amd import grid_fusion, hash_fusion, scene
+
+
+def main():
+    nd = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    passes = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    poses = scene.trajectory(nd, seed=0, radius_frac=scene.BENCH_RING)
+    d, c = scene.render(poses, scene.make_spheres(0, ring_frac=scene.BENCH_RING), seed=0,
+                        device=torch.device("cuda", 0), depth_dtype=torch.int16)
+    d64 = d.cpu().numpy().view(np.uint16).astype(np.float64) / 1000.0
+    ch = c.cpu().numpy()
+    K = scene.intrinsics()
+    out = {"copy_threads": os.environ.get("TSDF_COPY_THREADS", "default")}
+    for name, mk in (("dense", lambda: grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.02)),
+                     ("hash", lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
+                                                            max_blocks=1 << 15))):
+        v = mk()
+        v.integrate(ch[0], d64[0], K, poses[0])
+        v.sync()
+        rates = []
+        for _ in range(passes):
+            t0 = time.perf_counter()
+            for i in range(nd):
+                v.integrate(ch[i], d64[i], K, poses[i])
+            v.sync()
+            rates.append(round(nd / (time.perf_counter() - t0), 1))
+        out[name] = rates
+        v.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,9 +1,15 @@
 // tsdf_common.hip -- errors, device discovery, frame staging, pyramid launch, profiling and
 // the bulk hash_function entry point of the C-ABI (include/tsdf_hip.h).
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <thread>
+#include <vector>
 
 #include "tsdf_host.h"
 
@@ -238,13 +244,94 @@ static void frustum_planes(Frame* fr, const double* T, int W, int H) {
 }
 
 // memcpy with up to 8 threads (host bounce copies run at several times one core's bandwidth)
+// Host copies into the page-locked bounce slots (ingest and the deferred drop-in frames) by a
+// persistent pool of copy threads: one 640x480 f64 depth frame is 2.4 MB, and a single-thread
+// memcpy of it and its colour (~140 us) bounded the per-frame drop-in rate (6k frames/s; 10k
+// with the pool); spawning threads per call cost more than it saved below 4 MB.  The caller copies one share itself; the workers wake
+// on a generation counter.  TSDF_COPY_THREADS sets the pool size (0: copy on the calling thread).
+namespace {
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static std::mutex mk;
+        static CopyPool* pool = nullptr;
+        std::lock_guard<std::mutex> g(mk);
+        if (!pool || pool->pid_ != getpid()) pool = new CopyPool();  // (a forked child starts over;
+        return *pool;                                                  //  the parent's pool is left)
+    }
+    void copy(void* dst, const void* src, size_t bytes) {
+        const int nw = (int)workers_.size();
+        if (nw == 0 || bytes < (256u << 10)) {
+            std::memcpy(dst, src, bytes);
+            return;
+        }
+        std::lock_guard<std::mutex> call(call_);  // one copy at a time through the pool
+        const size_t parts = (size_t)nw + 1;
+        const size_t chunk = ((bytes + parts - 1) / parts + 63) & ~(size_t)63;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            dst_ = (char*)dst;
+            src_ = (const char*)src;
+            bytes_ = bytes;
+            chunk_ = chunk;
+            left_ = nw;
+            ++gen_;
+        }
+        cv_.notify_all();
+        std::memcpy(dst, src, std::min(chunk, bytes));  // share 0 on the calling thread
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [&] { return left_ == 0; });
+    }
+
+  private:
+    CopyPool() : pid_(getpid()) {
+        // two workers (three shares): 12.3k frames/s per-frame dense drop-in against 7.2k on the
+        // calling thread alone; four or eight were no faster and dipped more often
+        // (tools/gpu/dropin_rate.py, profiles/r02_dropin_copy_threads.txt)
+        int n = (int)std::min(2u, std::max(1u, std::thread::hardware_concurrency() / 2));
+        if (const char* e = getenv("TSDF_COPY_THREADS")) n = std::max(0, std::min(32, atoi(e)));
+        for (int i = 0; i < n; ++i) workers_.emplace_back([this, i] { run(i + 1); });
+        for (auto& t : workers_) t.detach();  // live for the process
+    }
+    void run(int share) {
+        unsigned long long seen = 0;
+        for (;;) {
+            char* d;
+            const char* s;
+            size_t bytes, chunk;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                d = dst_, s = src_, bytes = bytes_, chunk = chunk_;
+            }
+            const size_t o = (size_t)share * chunk;
+            if (o < bytes) std::memcpy(d + o, s + o, std::min(chunk, bytes - o));
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    pid_t pid_;
+    std::vector<std::thread> workers_;
+    std::mutex call_, m_;
+    std::condition_variable cv_, done_;
+    char* dst_ = nullptr;
+    const char* src_ = nullptr;
+    size_t bytes_ = 0, chunk_ = 0;
+    int left_ = 0;
+    unsigned long long gen_ = 0;
+};
+}  // namespace
+
 static void par_memcpy(void* dst, const void* src, size_t bytes) {
-    const unsigned hw = std::thread::hardware_concurrency();
-    const size_t nt = bytes < (4u << 20) ? 1 : std::min<size_t>(8, hw ? hw : 1);
-    if (nt <= 1) {
-        std::memcpy(dst, src, bytes);
+    if (bytes < (4u << 20)) {  // one frame (the drop-in's deferred frames): the pool
+        CopyPool::get().copy(dst, src, bytes);
         return;
     }
+    // whole batches (>= 4 MB): threads of their own -- measured faster than the pool here
+    // (pcie_inclusive 8.5-8.9k frames/s against 7.0-7.3k through the pool)
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nt = std::min<size_t>(8, hw ? hw : 1);
     std::vector<std::thread> th;
     const size_t chunk = (bytes + nt - 1) / nt;
     for (size_t i = 0; i < nt; ++i) {
