@@ -101,6 +101,14 @@ struct tsdf_hash {
     PoolState host_st{};
     ListEntry* d_list = nullptr;  // re-run list
     int list_cap = 0;
+    // A deferred batch launched by the drop-in's per-frame calls (TSDF_DEFER) whose overflow check
+    // waits for the next call on the handle (hash_settle): its frames and prepped buffers stay
+    // untouched until then, so a skipped brick is still re-run exactly, before any later frame.
+    struct Pending {
+        bool on = false;
+        Batch bt;
+        int dk = 0, ck = 0;
+    } pend;
     bool fused = true;  // three-stage launches (k_fused_hash) when a call allows them
     // Asynchronous calls (TSDF_ASYNC): every allocating launch reports its pool state into
     // page-locked host memory (PoolReport, slot seq % kReports); before issuing launch s the host
@@ -661,10 +669,15 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
 // before launch L+1 is issued; its re-run reads batch L's frames, which no launch has replaced.
 // The cull of batch L+1 already ran, which a resize cannot invalidate: it reads the table only
 // for shard ownership, fixed at create (Table::shard_cap).
+// Internal flag of hash_run: a synchronous call of at most one batch whose overflow check
+// (hash_after_batch + ensure_room) is left to the next call on the handle (hash_settle).
+constexpr int kCheckLater = 1 << 30;
+
 int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int H, int W,
                    const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     const bool sync = !(flags & TSDF_ASYNC);
+    const bool later = sync && (flags & kCheckLater) && n_frames <= kMaxBatch;
     TSDF_TRY(B.use_sets(kSets));
     const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedWG);
@@ -719,7 +732,13 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         if (!has_i) continue;
         TSDF_TRY(B.prof.end(B.stream, e0));
         B.frames += bi.n;
-        if (sync) {
+        if (later) {
+            TSDF_TRY(B.end_batch(flags, L % kSlots));
+            h->pend.bt = bi;
+            h->pend.dk = dk;
+            h->pend.ck = TSDF_COLOR_RGB8;
+            h->pend.on = true;
+        } else if (sync) {
             TSDF_TRY(hash_after_batch(h, bi, dk, TSDF_COLOR_RGB8));
             TSDF_TRY(B.end_batch(flags, L % kSlots));
             TSDF_TRY(ensure_room(h, true));
@@ -748,7 +767,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     if (fused) {
         TSDF_TRY(hash_run_fused(h, n_frames, depth, dk, color, H, W, K, Tinv, flags));
         TSDF_TRY(guard.finish());
-        if (sync) TSDF_HIP(hipStreamSynchronize(B.stream));
+        if (sync && !h->pend.on) TSDF_HIP(hipStreamSynchronize(B.stream));
         return TSDF_OK;
     }
     B.use_set(0);
@@ -785,17 +804,35 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     return TSDF_OK;
 }
 
-// Run the deferred frames (TSDF_DEFER) as one batch from their bounce slot, synchronously: a
-// full table or pool is then grown and the skipped bricks re-run exactly (hash_after_batch).
-int hash_flush(tsdf_hash* h) {
+// The pending deferred batch's overflow check: grow the table / pool and re-run its skipped
+// bricks exactly (hash_after_batch), then the load-factor policy.  Nothing has been launched on
+// the handle since that batch, so its frames and prepped buffers are intact.
+int hash_settle(tsdf_hash* h) {
+    if (!h->pend.on) return TSDF_OK;
+    h->pend.on = false;
+    TSDF_TRY(hash_after_batch(h, h->pend.bt, h->pend.dk, h->pend.ck));
+    TSDF_TRY(ensure_room(h, true));
+    return TSDF_OK;
+}
+
+// Run the deferred frames (TSDF_DEFER) as one batch from their bounce slot.  wait: synchronously
+// (every entry point before it touches the state); otherwise (the per-frame integrate that filled
+// the batch) the overflow check is left to the next call, so the host collects the next frames
+// while the GPU integrates these -- either way a full table or pool is grown and the skipped
+// bricks re-run exactly before any later frame is integrated.
+int hash_flush(tsdf_hash* h, bool wait = true) {
     Base& B = h->b;
+    TSDF_TRY(hash_settle(h));
     if (B.dfr.n == 0) return TSDF_OK;
     const Base::Deferred d = B.dfr;
     B.dfr.n = 0;
     B.prestaged = d.slot;
-    const int r = hash_run(h, d.n, B.hst_depth[d.slot], d.dk, B.hst_color[d.slot], d.ck, d.H, d.W, d.K, d.T, 0);
+    const int r = hash_run(h, d.n, B.hst_depth[d.slot], d.dk, B.hst_color[d.slot], d.ck, d.H, d.W, d.K, d.T,
+                           wait ? 0 : kCheckLater);
     B.prestaged = -1;
-    return r;
+    TSDF_TRY(r);
+    if (wait) TSDF_TRY(hash_settle(h));
+    return TSDF_OK;
 }
 
 int upload(tsdf_hash* h, const void* src, size_t bytes, void** dst) {
@@ -959,6 +996,7 @@ int tsdf_hash_reset(tsdf_hash_t* h) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     Base& B = h->b;
     B.dfr.n = 0;  // deferred frames are dropped with the state
+    h->pend.on = false;
     TSDF_HIP(hipSetDevice(B.device));
     hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, h->t.keys, (long long)h->t.capacity);
     TSDF_HIP(hipGetLastError());
@@ -986,7 +1024,7 @@ int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const
         if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(hash_flush(h));
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1
         TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0));
-        if (B.dfr.n == kMaxBatch) TSDF_TRY(hash_flush(h));
+        if (B.dfr.n == kMaxBatch) TSDF_TRY(hash_flush(h, false));
         return TSDF_OK;
     }
     TSDF_TRY(hash_flush(h));
