@@ -56,14 +56,16 @@ def test_deferred_per_frame_integrate_matches_oracle():
 
 
 def test_deferred_hash_per_frame_matches_dense():
-    """HashTable.integrate per frame (deferred, flushed synchronously so a full table / pool
-    grows and the skipped bricks re-run exactly) equals the dense grid."""
+    """HashTable.integrate per frame (deferred: the call that fills a batch launches it, and the
+    next call checks it -- a full table / pool grows and the skipped bricks re-run exactly before
+    any later frame) equals the dense grid; 29 frames = three such checks by per-frame calls and
+    one by the read."""
     from tsdf_amd import grid_fusion, hash_fusion
-    d, c, poses = _synth(13, start=610)
+    d, c, poses = _synth(29, start=610)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     g = grid_fusion.TSDFVolume(np.array(BNDS), 0.08, defer=False)
     h = hash_fusion.HashTable(np.array(BNDS), 0.08, 37, max_blocks=16)
-    for f in range(13):
+    for f in range(29):
         m = d[f].astype(float) / 1000.0
         g.integrate(c[f], m, K, poses[f])
         h.integrate(c[f], m, K, poses[f])

@@ -2,8 +2,9 @@
 
   * config[3] per rank: cyclic column shard 3 of 8 of the 512^3 @ 2 cm volume over 1000 frames
     of the bench trajectory, bit-exact against the oracle on rows of the shard;
-  * the fast-path boundary: weights around the 4087 limit of the LDS reciprocal table
-    (small_int, csrc/tsdf_device.h) and non-canonical colours, preloaded with set_state;
+  * the fast-path boundaries: weights around the 4087 limit of the LDS part of the reciprocal
+    table and the 65527 limit of the whole table (kRcpTab / kRcpBig, csrc/tsdf_device.h) and
+    non-canonical colours, preloaded with set_state;
   * config[4] per rank: bucket-range hash shard 5 of 8 over a 1024^3 @ 1 cm extent with 2^22
     buckets, against dense slabs (and the oracle) on rows restricted to the shard's blocks;
   * the hash's f32 state against the reference's float64 Voxel (voxel.py:19-49) over 500 frames,
@@ -69,12 +70,13 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
     assert w.max() >= 500 and vol.stats()["list_errors"] == 0
 
 
-@pytest.mark.parametrize("batched", [False, True])
-def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched):
-    """Preloaded weights 4078..4100 (the LDS table of RN(1/n) covers integer weights below 4087:
-    small_int switches the quotients to IEEE division mid-run) and colours that are not the
-    canonical B*65536+G*256+R integers (non-integral, negative, >= 2^24), next to canonical ones:
-    every path of the update equals the oracle bit for bit."""
+@pytest.mark.parametrize("batched,w_lo,limit", [(False, 4078, 4087), (True, 4078, 4087),
+                                                (True, 65515, 65527)])
+def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched, w_lo, limit):
+    """Preloaded weights around a limit of the RN(1/n) table (its LDS part covers integer weights
+    below 4087, then waves read the HBM part; past 65527 the quotients switch to IEEE division)
+    and colours that are not the canonical B*65536+G*256+R integers (non-integral, negative,
+    >= 2^24), next to canonical ones: every path of the update equals the oracle bit for bit."""
     from tsdf_amd import grid_fusion, scene
     n = 12
     depth, rgb, poses = _frames_on_device(n, start=120, ring=0.34)
@@ -85,7 +87,7 @@ def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched):
     orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
     shape = tuple(int(x) for x in vol._vol_dim)
     rng = np.random.default_rng(11)
-    w0 = rng.integers(4078, 4101, size=shape).astype(np.float32)
+    w0 = rng.integers(w_lo, w_lo + 23, size=shape).astype(np.float32)
     w0[rng.random(shape) < 0.3] = 0.0
     t0 = rng.uniform(-1, 1, size=shape).astype(np.float32)
     canon = (rng.integers(0, 256, size=shape) * 65536 + rng.integers(0, 256, size=shape) * 256
@@ -102,7 +104,7 @@ def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched):
         for f in range(n):
             vol.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
     T, W, C = vol.get_state()
-    assert (W > 4087).any() and (W[W > 0] < 4087).any()
+    assert (W > limit).any() and (W[W > 0] < limit).any()
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
 
 

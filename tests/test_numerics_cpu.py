@@ -36,7 +36,7 @@ def test_frustum_planes_contain_the_valid_pixel_range():
 
 def test_markstein_quotient_matches_ieee_division(tmp_path):
     """tsdf_device.h div_rn (RN(1/b) + one FMA correction) must equal a / b on the operand
-    ranges of the integrate kernels: diff / trunc and (w*t + dist) / (w + 1) for w < 4096."""
+    ranges of the integrate kernels: diff / trunc and (w*t + dist) / (w + 1) for w < 65536."""
     exe = os.path.join(tmp_path, "cm")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(REPO, "tools", "check_markstein.c"),
                     "-o", exe, "-lm"], check=True)
@@ -46,10 +46,10 @@ def test_markstein_quotient_matches_ieee_division(tmp_path):
 
 def test_f32_reciprocal_table_is_correctly_rounded():
     """The colour fast path takes RN32(1/n) as f32(RN64(1/n)) from the kernels' f64 table
-    (n < kRcpTab = 4096); double rounding must not change any entry."""
+    (n < kRcpBig = 65536); double rounding must not change any entry."""
     from fractions import Fraction
     import numpy as np
-    for n in range(1, 4096):
+    for n in range(1, 65536):
         y32 = np.float32(np.float64(1.0) / np.float64(n))
         exact = Fraction(1, n)
         # y32 is RN32(1/n) iff no other float32 is closer (ties: even mantissa)

@@ -2,8 +2,9 @@
  * q0 = RN(a*y), r = fma(-q0, b, a), q = fma(r, y, q0) equals the IEEE quotient a / b.
  *   (1) dist = diff / trunc for the truncation margins of every tested volume, diff over the
  *       integrate range [-trunc, 70 m] (random, plus values next to multiples of trunc);
- *   (2) tsdf = (w*t + dist) / (w + 1) for integer weights 1..4095 (the LDS table), numerators
- *       over [-4097, 4097] (random, plus values next to multiples of the divisor).
+ *   (2) tsdf = (w*t + dist) / (w + 1) for integer weights 1..65535 (the reciprocal table, LDS
+ *       part < 4096 and HBM part), numerators over [-(w+2), w+2] (random, plus values next to
+ *       multiples of the divisor).
  * Prints "markstein checked N mismatches M" (expected M = 0).  Build: gcc -O2 -ffp-contract=off -lm. */
 #include <math.h>
 #include <stdint.h>
@@ -41,9 +42,10 @@ int main(void) {
             }
         }
     }
-    for (int w = 1; w < 4096; ++w) {
-        const double b = (double)w, y = 1.0 / b;
-        for (int i = 0; i < 2000; ++i, ++n) bad += check(-4097.0 + 8194.0 * urand(), b, y);
+    for (int w = 1; w < 65536; ++w) {
+        const double b = (double)w, y = 1.0 / b, span = b + 2.0;
+        const int nr = w < 4096 ? 2000 : 150;
+        for (int i = 0; i < nr; ++i, ++n) bad += check(-span + 2.0 * span * urand(), b, y);
         for (int k = -w - 1; k <= w + 1; k += 1 + w / 64) {
             double a = (double)k * b + 0.5 * b * (k & 1);
             for (int j = 0; j < 6; ++j, ++n) {

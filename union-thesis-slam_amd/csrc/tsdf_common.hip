@@ -110,7 +110,7 @@ __global__ void k_zero_u64(unsigned long long* p, int n) {
 namespace {
 __global__ void k_fill_rcp(double* r) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kRcpTab) r[i] = 1.0 / (double)i;  // IEEE division: RN(1/i) (r[0] = inf, unused)
+    if (i < kRcpBig) r[i] = 1.0 / (double)i;  // IEEE division: RN(1/i) (r[0] = inf, unused)
 }
 }  // namespace
 
@@ -155,8 +155,8 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
     TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * kCountWords, stream));
     use_set(0);
-    TSDF_HIP(hipMalloc(&rcp, sizeof(double) * kRcpTab));
-    hipLaunchKernelGGL(k_fill_rcp, dim3((kRcpTab + 255) / 256), dim3(256), 0, stream, rcp);
+    TSDF_HIP(hipMalloc(&rcp, sizeof(double) * kRcpBig));
+    hipLaunchKernelGGL(k_fill_rcp, dim3((kRcpBig + 255) / 256), dim3(256), 0, stream, rcp);
     TSDF_HIP(hipGetLastError());
     vol.rcp = rcp;
     TSDF_HIP(hipMalloc(&stats, sizeof(unsigned long long) * kNStat * kStatSpread));

@@ -40,7 +40,7 @@ struct Vol {
     float origin[3];
     double vs, trunc;
     double rtrunc;  // RN(1 / trunc), from the host's IEEE division (Markstein quotient, below)
-    const double* rcp;  // kRcpTab entries RN(1/n) in HBM (copied to LDS by k_integrate)
+    const double* rcp;  // kRcpBig entries RN(1/n) in HBM (the first kRcpTab copied to LDS)
 };
 
 // Per-frame constants (by value).
@@ -83,10 +83,17 @@ static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
 // (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
 constexpr int kCountWords = 32, kDoneWord = 24;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
+// The whole table in HBM (512 KB, L2-resident) for waves with a weight past the LDS part (long
+// runs: weights pass 4087 after ~4300 frames of a room seen from inside); 65536 keeps every colour
+// numerator w*c + c' below 2^24 (exact in f32).
+constexpr int kRcpBig = 65536;
 
 // w is an integer small enough that w + kMaxBatch indexes the reciprocal table
 __device__ inline bool small_int(float w) {
     return w >= 0.0f && w < (float)(kRcpTab - kMaxBatch - 1) && w == truncf(w);
+}
+__device__ inline bool table_int(float w) {  // ... that indexes the HBM table
+    return w >= 0.0f && w < (float)(kRcpBig - kMaxBatch - 1) && w == truncf(w);
 }
 // a canonical folded colour: an integer B*65536 + G*256 + R in [0, 2^24) (what integrate writes)
 __device__ inline bool canon_color(float c) {
@@ -521,6 +528,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     unsigned nupd = 0;  // this lane's voxel updates: one v_bcnt per frame (a per-step count, or a
                         // wave-level ballot count, costs more VALU)
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
+    bool w_table = true;   // ... < kRcpBig
     bool c_canon = true;   // all loaded colours are canonical (canon_color)
 
 #ifdef TSDF_DIAG
@@ -657,6 +665,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             const float4 C = *(const float4*)(pool.color + base + 4 * h);
             ws[4 * h + 0] = W.x; ws[4 * h + 1] = W.y; ws[4 * h + 2] = W.z; ws[4 * h + 3] = W.w;
             w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
+            w_table = w_table && table_int(W.x) && table_int(W.y) && table_int(W.z) && table_int(W.w);
             c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
             ts[4 * h + 0] = T.x; ts[4 * h + 1] = T.y; ts[4 * h + 2] = T.z; ts[4 * h + 3] = T.w;
             cs[4 * h + 0] = C.x; cs[4 * h + 1] = C.y; cs[4 * h + 2] = C.z; cs[4 * h + 3] = C.w;
@@ -672,9 +681,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // LDS table and Markstein quotients; and, for RGB8 frames, every colour is canonical
         // (an integer B*65536+G*256+R < 2^24) -> the same for the three colour channels, in f32
         // with RN32(1/wn) = f32(RN64(1/wn)) (checked for every table entry by the CPU tests).
+        // Past the LDS part (a weight of the wave >= 4087) the same from the HBM table, in code of
+        // its own so the common path keeps its straight-line shape.
         const bool fast_t = OW1 && s_rcp && __ballot(!w_small) == 0;
-        const bool fast_c = CK == 0 && fast_t && __ballot(!c_canon) == 0;
-        float tq[NZ];
+        const bool table_t = OW1 && s_rcp && !fast_t && __ballot(!w_table) == 0;
+        const bool fast_c = CK == 0 && (fast_t || table_t) && __ballot(!c_canon) == 0;
+        float tq[NZ], rws[NZ];  // rws: RN32(1/wn) for the colour quotients
         if (fast_t) {
 #pragma unroll
             for (int k = 0; k < NZ; ++k) {
@@ -682,6 +694,16 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const double y = s_rcp[(int)wn];
                 const double num = (double)(ws[k] * ts[k]) + dist[k];
                 tq[k] = (float)div_rn(num, (double)wn, y);
+                rws[k] = (float)y;
+            }
+        } else if (table_t) {
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) {
+                const float wn = ws[k] + 1.0f;
+                const double y = v.rcp[(int)wn];
+                const double num = (double)(ws[k] * ts[k]) + dist[k];
+                tq[k] = (float)div_rn(num, (double)wn, y);
+                rws[k] = (float)y;
             }
         } else {
 #pragma unroll
@@ -689,6 +711,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const float wn = OW1 ? ws[k] + 1.0f : (float)((double)ws[k] + fr.ow);
                 const double num = (double)(ws[k] * ts[k]) + (OW1 ? dist[k] : fr.ow * dist[k]);
                 tq[k] = (float)(num / (double)wn);
+                rws[k] = 0.0f;
             }
         }
 #pragma unroll
@@ -711,12 +734,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             }
             float cn;
             if (fast_c) {
-                // canonical colours and integer weights < 4096: decode by bytes, exact integer
+                // canonical colours and integer weights < 65528: decode by bytes, exact integer
                 // numerators by FMA, Markstein quotients (b, g packed); every value is an integer
                 // < 2^24, so each step equals the reference's f32 expression, and the average is
                 // <= 255, so min(255, .) is a no-op
                 const unsigned cu = (unsigned)cs[k];
-                const float rw = (float)s_rcp[(int)wn];
+                const float rw = rws[k];
                 const float2 o_bg = make_float2((float)((cu >> 16) & 0xFFu), (float)((cu >> 8) & 0xFFu));
                 const float o_r = (float)(cu & 0xFFu);  // v_cvt_f32_ubyte{0,1,2}
                 const float2 n_bg = make_float2(nb, ng);
