@@ -50,7 +50,10 @@ extern "C" {
                                staging batch and return; the batch runs (asynchronously, as one
                                temporally batched launch) once it holds 8 frames or at the next
                                other call on the handle -- the reference's one-integrate()-per-
-                               frame loop (grid_demo1.py:76-87) at batched speed, same results */
+                               frame loop (grid_demo1.py:76-87) at batched speed, same results.
+                               Hash: a full table / pool found after a deferred batch is grown
+                               and its skipped bricks re-run at the next call, before anything
+                               else runs (exact, as for synchronous calls) */
 
 typedef struct tsdf_dense tsdf_dense_t;
 typedef struct tsdf_hash tsdf_hash_t;
