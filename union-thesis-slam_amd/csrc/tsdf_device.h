@@ -890,7 +890,8 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, Li
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
-                                      int n_waves, unsigned long long* s_stat, const double* s_rcp) {
+                                      int n_waves, unsigned long long* s_stat, const double* s_rcp,
+                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
@@ -912,6 +913,24 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
     }
     int c = kMaxBatch - 1;
     unsigned k0 = 0;  // list ordinal where class c starts (classes visited in descending order)
+    if (s_next) {
+        // Items dealt round-robin to workgroups (item e to workgroup e mod n_wg, still longest
+        // first) and taken dynamically by the workgroup's waves from an LDS counter: a wave that
+        // drew short items takes more, so a workgroup ends when its last item does, not when its
+        // unluckiest wave's static share does (the tail of small shards: few items per wave).
+        for (;;) {
+            unsigned j = 0;
+            if (lane_id() == 0) j = atomicAdd(s_next, 1u);
+            j = __builtin_amdgcn_readfirstlane(j);
+            const long long e = (long long)wg + (long long)j * n_wg;  // increasing for this wave
+            if (e >= (long long)total * parts) break;
+            const unsigned k = (unsigned)(e / parts);
+            while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
+            integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
+                                                   (int)(e % parts) * NZ, s_stat, s_rcp);
+        }
+        return;
+    }
     for (int e = wave; e < total * parts; e += n_waves) {
         const unsigned k = (unsigned)(e / parts);
         while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
@@ -937,14 +956,16 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_W
                                                   unsigned int* count, int n_list) {
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ double s_rcp[OW1 ? kRcpTab : 1];  // RN(1/n): weights are small integers when ow == 1
+    __shared__ unsigned s_next;                  // the workgroup's next list item (integrate_list)
     const int tid = threadIdx.x;
     if (tid < kNStat) s_stat[tid] = 0;
+    if (tid == 0) s_next = 0;
     if (OW1)  // 32 KB table copied with 16-byte loads (computing it cost 16 f64 divisions per thread)
         for (int i = tid; i < kRcpTab / 2; i += kWG) ((double2*)s_rcp)[i] = ((const double2*)v.rcp)[i];
     __syncthreads();
     integrate_list<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list, count, n_list,
                                           blockIdx.x * (kWG / 64) + (tid >> 6), gridDim.x * (kWG / 64),
-                                          s_stat, OW1 ? s_rcp : nullptr);
+                                          s_stat, OW1 ? s_rcp : nullptr, &s_next, blockIdx.x, gridDim.x);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
@@ -1124,17 +1145,19 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     // integrate: RN(1/n) table; cull: per-brick frame masks; prep: two pyramid tiles
     __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
+    __shared__ unsigned s_next;
     const int tid = threadIdx.x, b = blockIdx.x;
     const Table no_table{};
     if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
+        if (tid == 0) s_next = 0;
         if (OW1)
             for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedWG / 64;
         integrate_list<false, DK, 0, OW1, NZ>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
-                                             OW1 ? s_buf : nullptr);
+                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
@@ -1179,14 +1202,16 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_H
     __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ int s_last;
+    __shared__ unsigned s_next;
     const int tid = threadIdx.x, b = blockIdx.x;
     if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
+        if (tid == 0) s_next = 0;
         for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedWG / 64;
         integrate_list<true, DK, 0, true, 8>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
-                                            sg.gi * wpg, s_stat, s_buf);
+                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi);
         __syncthreads();
         flush_stats(s_stat, stats);
         if (tid == 0) {
