@@ -1000,9 +1000,10 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
     float* pyr = (float*)fr.pyr;
     const int t = threadIdx.x, r = t >> 4, c = t & 15;
     if (count && t < kCountWords && tx == 0 && ty == 0 && tf == 0) coh_store(count + t, 0u);  // list counters
+    const bool act = t < 512;  // (a fused launch's workgroup may be larger: the rest only meets the barriers)
     const int x0 = tx * 64 + c * 4, y0 = ty * 64 + r * 2;
     float ma = 0.0f, mb = 0.0f;  // level-1 texels (x0/2, y0/2) and (x0/2 + 1, y0/2)
-    if (x0 < fr.W) {
+    if (act && x0 < fr.W) {
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy) {
             const int y = y0 + dy;
@@ -1033,16 +1034,16 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
                 make_uint4(a & 0xFFFFFFu, (a >> 24) | ((b & 0xFFFFu) << 8), (b >> 16) | ((cc & 0xFFu) << 16), cc >> 8);
         }
     }
-    {
+    if (act) {
         const int X = x0 >> 1, Y = y0 >> 1;
         const PyrGeo& pg = bt.pg;
         if (Y < pg.h[1]) {
             if (X < pg.w[1]) pyr[pg.off[1] + Y * pg.w[1] + X] = ma;
             if (X + 1 < pg.w[1]) pyr[pg.off[1] + Y * pg.w[1] + X + 1] = mb;
         }
+        sa[r][2 * c] = ma;
+        sa[r][2 * c + 1] = mb;
     }
-    sa[r][2 * c] = ma;
-    sa[r][2 * c + 1] = mb;
     __syncthreads();
     pyr_level<0>(bt.pg, pyr, 2, sa, sb, 16, tx, ty);
     __syncthreads();
@@ -1125,8 +1126,17 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
 // integrate workgroups come first in dispatch order; the cull and prep workgroups take the CUs
 // its tail frees.  One launch per batch replaces three kernels and the gaps between them.
 // ---------------------------------------------------------------------------------------------
-constexpr int kFusedWG = 512;
-static_assert(kFusedWG == kCullWG, "a cull workgroup is one wave per frame of the batch");
+// Fused workgroups: the integrate's waves share one dynamic item pool per workgroup, so larger
+// workgroups balance better; the cull and prep stages use the first 512 threads.
+#ifndef TSDF_FUSED_WG
+#define TSDF_FUSED_WG 768  // dense: 12 waves, 2 per CU at 6 waves/SIMD (+0.8 % over 512)
+#endif
+#ifndef TSDF_FUSED_HASH_WG
+#define TSDF_FUSED_HASH_WG 512
+#endif
+constexpr int kFusedWG = TSDF_FUSED_WG, kFusedHashWG = TSDF_FUSED_HASH_WG;
+static_assert(kFusedWG >= kCullWG && kFusedHashWG >= kCullWG && kFusedWG % 64 == 0 && kFusedHashWG % 64 == 0,
+              "a cull workgroup is one wave per frame of the batch");
 struct Stage {
     const ListEntry* list_i;  // integrate: list and count of batch k
     unsigned int* count_i;
@@ -1197,7 +1207,7 @@ __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolRepo
 // commit done by the integrate workgroup that finishes last (an arrival counter in the batch's
 // list counters; every workgroup's allocations are complete before it arrives).
 template <int DK = 0>
-__global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_fused_hash(
+__global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_fused_hash(
         Vol v, Batch bi, Batch bc, Batch bp, Pool pool, Table tab, unsigned long long* stats, Stage sg) {
     __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
@@ -1207,9 +1217,9 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_H
     if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
         if (tid == 0) s_next = 0;
-        for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
+        for (int i = tid; i < kRcpTab / 2; i += kFusedHashWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
-        constexpr int wpg = kFusedWG / 64;
+        constexpr int wpg = kFusedHashWG / 64;
         integrate_list<true, DK, 0, true, 8>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
                                             sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi);
         __syncthreads();

@@ -680,7 +680,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     const bool later = sync && (flags & kCheckLater) && n_frames <= kMaxBatch;
     TSDF_TRY(B.use_sets(kSets));
     const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
-    const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedWG);
+    const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
     const int gc_full = (int)B.cull_grid();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
@@ -723,10 +723,10 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
         if (dk == TSDF_DEPTH_U16_MM)
-            hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, bc,
+            hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, B.vol, bi, bc,
                                bp, B.pool, h->t, B.stats, sg);
         else
-            hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, bi, bc,
+            hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, B.vol, bi, bc,
                                bp, B.pool, h->t, B.stats, sg);
         TSDF_HIP(hipGetLastError());
         if (!has_i) continue;
