@@ -914,20 +914,22 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
     int c = kMaxBatch - 1;
     unsigned k0 = 0;  // list ordinal where class c starts (classes visited in descending order)
     if (s_next) {
-        // Items dealt round-robin to workgroups (item e to workgroup e mod n_wg, still longest
-        // first) and taken dynamically by the workgroup's waves from an LDS counter: a wave that
+        // Items dealt round-robin to workgroups (still longest first) and taken dynamically by
+        // the workgroup's waves from an LDS counter: a wave that
         // drew short items takes more, so a workgroup ends when its last item does, not when its
         // unluckiest wave's static share does (the tail of small shards: few items per wave).
         for (;;) {
             unsigned j = 0;
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
-            const long long e = (long long)wg + (long long)j * n_wg;  // increasing for this wave
-            if (e >= (long long)total * parts) break;
-            const unsigned k = (unsigned)(e / parts);
-            while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
-            integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
-                                                   (int)(e % parts) * NZ, s_stat, s_rcp);
+            // bricks dealt to workgroups (brick k to workgroup k mod n_wg), the parts of one brick
+            // taken one after the other, so they run side by side on the workgroup's waves and
+            // share their depth / colour gathers in the CU's cache
+            const long long k = (long long)wg + (long long)(j / parts) * n_wg;  // increasing for this wave
+            if (k >= (long long)total) break;
+            while (c > 0 && (unsigned)k - k0 >= ncls[c]) k0 += ncls[c--];
+            integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
+                                                   (int)(j % parts) * NZ, s_stat, s_rcp);
         }
         return;
     }
