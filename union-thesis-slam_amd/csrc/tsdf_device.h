@@ -14,6 +14,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace tsdf {
 
@@ -150,6 +151,7 @@ struct Table {
 };
 
 // hash_function (hash_fusion.py:182-190): ((x*P1) ^ (y*P2) ^ (z*P3)) floor-mod n.
+template <bool POW2 = false>  // POW2: n is a power of two (the fused hash launch; no division code)
 __host__ __device__ inline long long ref_hash(long long x, long long y, long long z, long long n,
                                               int int_bits) {
     const unsigned long long P1 = 73856093ull, P2 = 19349669ull, P3 = 83492791ull;
@@ -166,14 +168,15 @@ __host__ __device__ inline long long ref_hash(long long x, long long y, long lon
     // floor-mod; a power-of-two n (the bench's 2^22 buckets) by a mask -- the same residue for
     // negative h in two's complement -- instead of a 64-bit division (hundreds of VALU
     // instructions per brick in the integrate and the sharded cull)
-    if ((n & (n - 1)) == 0) return h & (n - 1);
+    if (POW2 || (n & (n - 1)) == 0) return h & (n - 1);
     long long m = h % n;
     return m < 0 ? m + n : m;
 }
 
 // Shard owning home slot `home` of a table of `cap` slots (bucket ranges).
+template <bool POW2 = false>
 __host__ __device__ inline int shard_of(long long home, int n_shards, long long cap) {
-    if ((cap & (cap - 1)) == 0) return (int)((home * n_shards) >> (63 - __builtin_clzll((unsigned long long)cap)));
+    if (POW2 || (cap & (cap - 1)) == 0) return (int)((home * n_shards) >> (63 - __builtin_clzll((unsigned long long)cap)));
     return (int)((home * n_shards) / cap);
 }
 
@@ -480,11 +483,137 @@ __device__ inline unsigned halves_of(unsigned m) {
     return NZ == 8 ? (((m & 0x0Fu) ? 1u : 0u) | ((m & 0xF0u) ? 2u : 0u)) : (m ? 1u : 0u);
 }
 
+// Phases 1-3 of one frame for one part (z-steps zoff .. zoff+NZ-1 of a lane's column): project,
+// gather, depth / truncation test.  Returns the valid steps (bit k); fills the packed colour
+// texels and the clamped distances of every step.
+template <int DK, int CK, int NZ>
+__device__ __forceinline__ unsigned project_part(const Vol& v, const Frame& fr, double px, double py,
+                                                 const double* pzs, double pz_l, int zoff, bool col_in, int nz,
+                                                 unsigned (&cpx)[NZ], double (&dist)[NZ]) {
+    constexpr int kPz = NZ < 8 ? NZ : 1;
+    // x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:363-368)
+    const double a0 = fma(fr.T[1], py, fr.T[0] * px);
+    const double a1 = fma(fr.T[5], py, fr.T[4] * px);
+    const double a2 = fma(fr.T[9], py, fr.T[8] * px);
+    // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
+    // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
+    // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
+    // the pixel indices leave the f64 domain at once (saturating v_cvt_i32_f64: out-of-range
+    // values clamp to INT_MIN / INT_MAX and fail the unsigned bounds test below), which keeps
+    // two f64 per step out of the registers live across the gathers (no VGPR spill left)
+    double zc[NZ];
+    int iu[NZ], iv[NZ];
+    unsigned inb = 0, slow = 0;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
+        const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
+        const double x = fr.T[3] + fma(fr.T[2], pz, a0);
+        const double y = fr.T[7] + fma(fr.T[6], pz, a1);
+        const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see frame_margin
+        // one FMA for (x*fx)*rz + cx: within |u - cx| * 2^-24.3 of the reference's
+        // (x*fx)/z + cx, inside the frame_margin boundary margin below
+        const double sx = fma(x * fr.fx, rz, fr.cx), sy = fma(y * fr.fy, rz, fr.cy);
+        const double ux = rint(sx), uy = rint(sy);
+        // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
+        // but is invalid either way)
+        const bool ok = fabs(sx - ux) < fr.half_m && fabs(sy - uy) < fr.half_m;
+        const bool in = col_in && k < nz && z > 0.0;
+        zc[k] = z;
+        iu[k] = cvt_i32_sat(ux);
+        iv[k] = cvt_i32_sat(uy);
+        inb |= (unsigned)in << k;
+        slow |= (unsigned)(in && !ok) << k;
+    }
+    if (__ballot(slow != 0)) {
+#pragma unroll
+        for (int k = 0; k < NZ; ++k) {
+            if (!((slow >> k) & 1u)) continue;
+            const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
+            const double x = fr.T[3] + fma(fr.T[2], pz, a0);
+            const double y = fr.T[7] + fma(fr.T[6], pz, a1);
+            iu[k] = cvt_i32_sat(rint((x * fr.fx) / zc[k] + fr.cx));  // the reference's own operation order
+            iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
+        }
+    }
+    unsigned cand = 0;
+    unsigned pix[NZ];
+    const int W = fr.W, H = fr.H;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        // unsigned bounds on the saturated indices (they come from integral, non-NaN values
+        // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
+        // np.linalg.inv: all NaN -- fails z > 0)
+        const bool c = ((inb >> k) & 1u) && (unsigned)iu[k] < (unsigned)W && (unsigned)iv[k] < (unsigned)H;
+        cand |= (unsigned)c << k;
+        pix[k] = c ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
+    }
+    // phase 2: gather depth and colour for every step at once, before the depth test, so
+    // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
+    // scheduling barrier keeps the compiler from sinking each load next to its use, which
+    // under the 128-VGPR budget it otherwise does, serialising the latencies.
+    unsigned draw[NZ];
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        draw[k] = depth_raw<DK>(fr, pix[k]);
+        cpx[k] = texel<unsigned>(CK == 0 ? (const void*)fr.rgbx : fr.color, pix[k]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double dep[NZ];
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fr, pix[k], draw[k]);
+    // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
+    unsigned vmask = 0;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        const double diff = dep[k] - zc[k];
+        const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
+        const double dd = div_rn(diff, v.trunc, v.rtrunc);
+        dist[k] = fmin(dd, 1.0);  // np.minimum(1, .) (dd is never NaN)
+        vmask |= (unsigned)ok << k;
+    }
+    return vmask;
+}
+
+// Hash z-half waves (NZ = 4, the fused hash launch).  The two halves of a brick are waves 2m and
+// 2m+1 of one workgroup (integrate_list with an even wave count per workgroup) and meet in the
+// brick's claim word of the batch (res[b], reset to kResFree by the cull that listed the brick):
+//  * at item start the z-low wave looks the block up (no insert) and publishes the block or
+//    kResMissing; the z-high wave waits for it.  Both then run the frame loop like the dense grid:
+//    no probe state is live inside the loop, so the hash integrate fits the dense grid's 80 VGPRs;
+//  * a missing block is allocated only if a half really updates a voxel: that half runs the frames
+//    up to its first valid voxel (a dry pass), claims the word (kResMissing -> kResBusy), inserts,
+//    initialises the other half and the entry words, publishes block | kResNew (or kResFail when
+//    the table or pool is full) and re-runs its frames; the other half, if it needs the block
+//    too, waits for the publication.  A claimer never waits, so every wait ends.
+// Both waves share a workgroup, so workgroup-scope ordering suffices (agent scope would write
+// back and invalidate the XCD's L2 at every claim).
+constexpr int kResFree = -1, kResBusy = -2, kResFail = -3, kResMissing = -4;
+constexpr int kResNew = 1 << 30;  // published block | kResNew: inserted by this launch (blocks < 2^30)
+
+__device__ inline int res_load(const int* rp) {
+    return __hip_atomic_load(rp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void res_publish(int* rp, int val) {  // lane 0, after the wave's stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane_id() == 0) __hip_atomic_store(rp, val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline int res_wait(const int* rp, int busy) {  // the published value once not `busy`
+    int cur = res_load(rp);
+    while (cur == busy) {
+        __builtin_amdgcn_s_sleep(1);
+        cur = res_load(rp);
+    }
+    return cur;
+}
+
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, ListEntry entry, int zoff,
-                                       unsigned long long* s_stat, const double* s_rcp) {
-    static_assert(NZ == 8 || (NZ == 4 && !HASH), "z-split parts are dense-only");
+                                       unsigned long long* s_stat, const double* s_rcp,
+                                       int* res = nullptr) {
+    static_assert(NZ == 8 || NZ == 4, "z-parts of 8 or 4 steps");
+    constexpr bool kHalfHash = HASH && NZ == 4;  // (requires res)
     constexpr unsigned kHalves = NZ == 8 ? 3u : 1u;
     const int lane = lane_id();
     const int b = (int)(entry & 0xFFFFFFFFull);
@@ -513,6 +642,91 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #pragma unroll
     for (int k = 0; k < kPz; ++k) pzs[k] = readlane_f64(pz_l, k + zoff);
 
+    // the brick's storage: dense brick b, or its hash pool block (wave-uniform; 32-bit for the hash,
+    // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
+    typename std::conditional<HASH, int, long long>::type blk = -1;
+    bool is_new = false;
+    if constexpr (kHalfHash) {
+        int* const rp = res + b;
+        int cur;
+        if (zoff == 0) {  // the z-low wave looks the block up for both halves
+            long long slot = 0, probe = 0;
+            const int r = table_find_or_insert(tab, pack_key(bx, by, bz), ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits),
+                                               false, is_new, slot, probe);
+            cur = r >= 0 ? r : kResMissing;
+            res_publish(rp, cur);
+            if (lane == 0) {
+                atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
+                atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
+                atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
+            }
+        } else {
+            cur = res_wait(rp, kResFree);
+        }
+        if (cur >= 0) {  // found, or (z-high wave) already inserted by its sibling
+            blk = cur & (kResNew - 1);
+            is_new = (cur & kResNew) != 0;
+        } else {  // missing: a dry pass up to this half's first valid voxel decides whether it needs one
+            bool need = false;
+            for (int fi = 0; fi < bt.n && !need; ++fi) {
+                if (!((fmask >> fi) & 1u)) continue;
+                unsigned cpx[NZ];
+                double dist[NZ];
+                const unsigned vm = project_part<DK, CK, NZ>(v, bt.f[fi], px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist);
+                need = __ballot(vm != 0) != 0;
+            }
+            if (!need) return;  // no frame of the batch updates this half
+            cur = res_load(rp);
+            bool claimer = false;
+            if (cur == kResMissing) {
+                int old = kResMissing;
+                if (lane == 0)
+                    __hip_atomic_compare_exchange_strong(rp, &old, kResBusy, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __shfl(old, 0);
+                claimer = old == kResMissing;
+                cur = old;
+            }
+            if (claimer) {
+                long long slot = 0, probe = 0;
+                const int r = table_find_or_insert(tab, pack_key(bx, by, bz),
+                                                   ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits), true, is_new,
+                                                   slot, probe);
+                if (r < 0) {  // no space: the brick waits for the host's re-run (nothing written)
+                    if (lane == 0) {
+                        const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
+                        if ((long long)o < tab.overflow_cap) tab.overflow[o] = entry;
+                        atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
+                    }
+                    res_publish(rp, kResFail);
+                    return;
+                }
+                if (is_new) {  // the other half and every entry word start fresh too
+                    const size_t pb = (size_t)r * kBrickVox + (size_t)lane * kBrickEdge + (4 - zoff);
+                    *(float4*)(pool.weight + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    *(float4*)(pool.tsdf + pb) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                    *(float4*)(pool.color + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    if (lane < kBrickEdge) coh_store(tab.occ + (size_t)r * kBrickEdge + lane, 0ull);
+                }
+                cur = r | (is_new ? kResNew : 0);
+                res_publish(rp, cur);
+                if (lane == 0) {
+                    atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
+                    atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
+                    if (is_new) atomicAdd(&s_stat[ST_ALLOC], 1ull);
+                }
+            } else {
+                cur = res_wait(rp, kResBusy);
+                if (cur == kResFail) return;
+            }
+            blk = cur & (kResNew - 1);
+            is_new = (cur & kResNew) != 0;
+        }
+        if (blk >= tab.max_blocks) {  // never: a published block is one of this launch's pool
+            if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
+            return;
+        }
+    }
     float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
@@ -520,11 +734,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         ts[k] = 1.0f;
         cs[k] = 0.0f;
     }
-    unsigned loaded = 0;   // 16-B halves of this lane's column held in registers (bit 0: z 0-3)
+    // 16-B halves of this lane's column held in registers (bit 0: z 0-3); a half of a block this
+    // launch inserted starts at (1, 0, 0): nothing to load
+    unsigned loaded = (kHalfHash && is_new) ? kHalves : 0u;
     unsigned dirty = 0;    // halves changed by the batch
     unsigned touched = 0;  // voxels updated by any frame of the batch (entry bits, hash)
-    long long blk = -1;
-    bool is_new = false;
     unsigned nupd = 0;  // this lane's voxel updates: one v_bcnt per frame (a per-step count, or a
                         // wave-level ballot count, costs more VALU)
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
@@ -540,98 +754,19 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #ifdef TSDF_DIAG
         ++d_pairs;
 #endif
-        // x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:363-368)
-        const double a0 = fma(fr.T[1], py, fr.T[0] * px);
-        const double a1 = fma(fr.T[5], py, fr.T[4] * px);
-        const double a2 = fma(fr.T[9], py, fr.T[8] * px);
-        // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
-        // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
-        // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
-        // the pixel indices leave the f64 domain at once (saturating v_cvt_i32_f64: out-of-range
-        // values clamp to INT_MIN / INT_MAX and fail the unsigned bounds test below), which keeps
-        // two f64 per step out of the registers live across the gathers (no VGPR spill left)
-        double zc[NZ];
-        int iu[NZ], iv[NZ];
-        unsigned inb = 0, slow = 0;
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) {
-            const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
-            const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
-            const double x = fr.T[3] + fma(fr.T[2], pz, a0);
-            const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-            const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see frame_margin
-            // one FMA for (x*fx)*rz + cx: within |u - cx| * 2^-24.3 of the reference's
-            // (x*fx)/z + cx, inside the frame_margin boundary margin below
-            const double sx = fma(x * fr.fx, rz, fr.cx), sy = fma(y * fr.fy, rz, fr.cy);
-            const double ux = rint(sx), uy = rint(sy);
-            // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
-            // but is invalid either way)
-            const bool ok = fabs(sx - ux) < fr.half_m && fabs(sy - uy) < fr.half_m;
-            const bool in = col_in && k < nz && z > 0.0;
-            zc[k] = z;
-            iu[k] = cvt_i32_sat(ux);
-            iv[k] = cvt_i32_sat(uy);
-            inb |= (unsigned)in << k;
-            slow |= (unsigned)(in && !ok) << k;
-        }
-        if (__ballot(slow != 0)) {
-#pragma unroll
-            for (int k = 0; k < NZ; ++k) {
-                if (!((slow >> k) & 1u)) continue;
-                const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
-                const double x = fr.T[3] + fma(fr.T[2], pz, a0);
-                const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-                iu[k] = cvt_i32_sat(rint((x * fr.fx) / zc[k] + fr.cx));  // the reference's own operation order
-                iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
-            }
-        }
-        unsigned cand = 0;
-        unsigned pix[NZ];
-        const int W = fr.W, H = fr.H;
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) {
-            // unsigned bounds on the saturated indices (they come from integral, non-NaN values
-            // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
-            // np.linalg.inv: all NaN -- fails z > 0)
-            const bool c = ((inb >> k) & 1u) && (unsigned)iu[k] < (unsigned)W && (unsigned)iv[k] < (unsigned)H;
-            cand |= (unsigned)c << k;
-            pix[k] = c ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
-        }
-        // phase 2: gather depth and colour for every step at once, before the depth test, so
-        // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
-        // scheduling barrier keeps the compiler from sinking each load next to its use, which
-        // under the 128-VGPR budget it otherwise does, serialising the latencies.
-        unsigned draw[NZ], cpx[NZ];
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) {
-            draw[k] = depth_raw<DK>(fr, pix[k]);
-            cpx[k] = texel<unsigned>(CK == 0 ? (const void*)fr.rgbx : fr.color, pix[k]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        double dep[NZ];
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fr, pix[k], draw[k]);
-        // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
-        unsigned vmask = 0;
+        unsigned cpx[NZ];
         double dist[NZ];
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) {
-            const double diff = dep[k] - zc[k];
-            const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
-            const double dd = div_rn(diff, v.trunc, v.rtrunc);
-            dist[k] = fmin(dd, 1.0);  // np.minimum(1, .) (dd is never NaN)
-            vmask |= (unsigned)ok << k;
-        }
+        const unsigned vmask = project_part<DK, CK, NZ>(v, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist);
         if (__ballot(vmask != 0) == 0) continue;
 #ifdef TSDF_DIAG
         ++d_valid;
 #endif
 
-        if (blk < 0) {  // first frame of the batch that updates this brick: find its storage
+        if (!kHalfHash && blk < 0) {  // first frame of the batch that updates this brick: find its storage
             if (HASH) {
                 long long slot = 0, probe = 0;
                 const unsigned long long key = pack_key(bx, by, bz);
-                const long long home = ref_hash(bx, by, bz, tab.capacity, tab.int_bits);
+                const long long home = ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits);
                 const int r = table_find_or_insert(tab, key, home, true, is_new, slot, probe);
                 if (r < 0) {  // no space: skip the brick for the whole batch (nothing written yet);
                     if (lane == 0) {  // the host grows the table and re-runs it
@@ -771,6 +906,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     }
 #endif
     if (blk < 0) return;  // no frame of the batch updated this brick
+    if (kHalfHash && __ballot(touched != 0) == 0) return;  // (its block was looked up in advance)
 
     // phase 6: store the changed halves once (a new hash block is written whole: its init)
     const unsigned st = dirty | ((HASH && is_new) ? kHalves : 0u);
@@ -782,15 +918,15 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         *(float4*)(pool.tsdf + base + 4 * h) = make_float4(ts[4 * h], ts[4 * h + 1], ts[4 * h + 2], ts[4 * h + 3]);
         *(float4*)(pool.color + base + 4 * h) = make_float4(cs[4 * h], cs[4 * h + 1], cs[4 * h + 2], cs[4 * h + 3]);
     }
-    if constexpr (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns the block this launch
+    if constexpr (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns words zoff .. zoff+NZ-1
         unsigned long long mine = 0;
 #pragma unroll
-        for (int k = 0; k < kBrickEdge; ++k) {
+        for (int k = 0; k < NZ; ++k) {
             const unsigned long long m = __ballot((touched >> k) & 1u);
             if (lane == k) mine = m;
         }
-        if (lane < kBrickEdge) {
-            unsigned long long* o = tab.occ + (size_t)blk * kBrickEdge + lane;
+        if (lane < NZ) {
+            unsigned long long* o = tab.occ + (size_t)blk * kBrickEdge + zoff + lane;
             if (is_new) coh_store(o, mine);
             else if (mine) atomicOr(o, mine);
         }
@@ -822,10 +958,10 @@ constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 
 // survives, each lane tests its brick against frame f; the per-brick frame masks meet in LDS and
 // wave 0 appends the kept bricks to the list (one atomicAdd per superbrick with survivors).
 // Every test is at most two cull_brick latencies deep, whatever the batch size.
-template <bool HASH>
+template <bool HASH, bool P2 = false>
 __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Table& tab, ListEntry* list,
                                        unsigned int* count, unsigned long long* stats, int si,
-                                       unsigned* s_mask, unsigned long long* s_stat) {
+                                       unsigned* s_mask, unsigned long long* s_stat, int* res = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int f0 = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid < 64) s_mask[tid] = 0u;
@@ -843,8 +979,8 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         if (cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
             bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
             if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership
-                const long long home = ref_hash(bx, by, bz, tab.shard_cap, tab.int_bits);
-                test = shard_of(home, v.n_shards, tab.shard_cap) == v.shard;
+                const long long home = ref_hash<P2>(bx, by, bz, tab.shard_cap, tab.int_bits);
+                test = shard_of<P2>(home, v.n_shards, tab.shard_cap) == v.shard;
             }
             if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
         }
@@ -867,8 +1003,10 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
             if (lane == 0) s_stat[ST_VISITED] = (unsigned long long)__popcll(any);
             base = __shfl(base, cls);
             const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
-            if (cls && base + rank < nbk)
+            if (cls && base + rank < nbk) {
                 list[(size_t)(cls - 1) * nbk + base + rank] = (ListEntry)e | ((ListEntry)fmask << 32);
+                if (HASH && res) res[e] = kResFree;  // the brick's claim word for this batch
+            }
         }
     }
     __syncthreads();
@@ -891,7 +1029,7 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1) {
+                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
@@ -928,8 +1066,9 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
             const long long k = (long long)wg + (long long)(j / parts) * n_wg;  // increasing for this wave
             if (k >= (long long)total) break;
             while (c > 0 && (unsigned)k - k0 >= ncls[c]) k0 += ncls[c--];
+            // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
             integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
-                                                   (int)(j % parts) * NZ, s_stat, s_rcp);
+                                                   (int)(j % parts) * NZ, s_stat, s_rcp, res);
         }
         return;
     }
@@ -937,7 +1076,7 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
         const unsigned k = (unsigned)(e / parts);
         while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
         integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
-                                               (e % parts) * NZ, s_stat, s_rcp);
+                                               (e % parts) * NZ, s_stat, s_rcp, res);
     }
 }
 
@@ -1148,6 +1287,8 @@ struct Stage {
     int gi, gc;              // integrate / cull workgroups
     int ptx, pty;            // prep tiles per frame (x, y)
     long long seq;           // hash: launch number for the pool report (Table::rb)
+    int* res_i;              // hash: per-brick claim words of batch k (integrate) and k+1 (cull)
+    int* res_c;
 };
 
 template <bool OW1, int NZ, int DK = 0>
@@ -1208,8 +1349,12 @@ __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolRepo
 // k_fused, with the hash integrate (one wave per brick, in-kernel find-or-insert) and the pool
 // commit done by the integrate workgroup that finishes last (an arrival counter in the batch's
 // list counters; every workgroup's allocations are complete before it arrives).
+// (z-half waves, two per brick)
+#ifndef TSDF_FUSED_HASH_WAVES
+#define TSDF_FUSED_HASH_WAVES 6
+#endif
 template <int DK = 0>
-__global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_fused_hash(
+__global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TSDF_FUSED_HASH_WAVES))) void k_fused_hash(
         Vol v, Batch bi, Batch bc, Batch bp, Pool pool, Table tab, unsigned long long* stats, Stage sg) {
     __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
@@ -1222,8 +1367,8 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         for (int i = tid; i < kRcpTab / 2; i += kFusedHashWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedHashWG / 64;
-        integrate_list<true, DK, 0, true, 8>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
-                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi);
+        integrate_list<true, DK, 0, true, 4>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
+                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i);
         __syncthreads();
         flush_stats(s_stat, stats);
         if (tid == 0) {
@@ -1236,7 +1381,8 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
             commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq);
         }
     } else if (b < sg.gi + sg.gc) {
-        cull_superbrick<true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf, s_stat);
+        cull_superbrick<true, true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
+                                    s_stat, sg.res_c);
     } else {
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;

@@ -101,6 +101,7 @@ struct tsdf_hash {
     PoolState host_st{};
     ListEntry* d_list = nullptr;  // re-run list
     int list_cap = 0;
+    int* d_res = nullptr;  // fused launches: per-brick claim words, one array per buffer set
     // A deferred batch launched by the drop-in's per-frame calls (TSDF_DEFER) whose overflow check
     // waits for the next call on the handle (hash_settle): its frames and prepped buffers stay
     // untouched until then, so a skipped brick is still re-run exactly, before any later frame.
@@ -680,6 +681,11 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     const bool later = sync && (flags & kCheckLater) && n_frames <= kMaxBatch;
     TSDF_TRY(B.use_sets(kSets));
     const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
+    if (!h->d_res) {  // each word is written by the cull that lists its brick before an integrate reads it
+        if (h->t.max_blocks >= kResNew || B.n_bricks >= (1ll << 31) / kSets)
+            return set_error(TSDF_E_ARG, "volume too large for the claim words");
+        TSDF_HIP(hipMalloc(&h->d_res, sizeof(int) * kSets * (size_t)B.n_bricks));
+    }
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
     const int gc_full = (int)B.cull_grid();
     Batch bts[kSets];
@@ -706,10 +712,12 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         if (has_i) {
             sg.list_i = B.list_set[L % kSets];
             sg.count_i = B.count_set[L % kSets];
+            sg.res_i = h->d_res + (size_t)(L % kSets) * B.n_bricks;
         }
         if (has_c) {
             sg.list_c = B.list_set[(L + 1) % kSets];
             sg.count_c = B.count_set[(L + 1) % kSets];
+            sg.res_c = h->d_res + (size_t)((L + 1) % kSets) * B.n_bricks;
         }
         if (has_p) sg.count_p = B.count_set[jp % kSets];
         const long long grid = (long long)sg.gi + sg.gc + (has_p ? (long long)sg.ptx * sg.pty * bp.n : 0);
@@ -760,7 +768,11 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
-    bool fused = h->fused && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0;
+    // (the fused launch is built for power-of-two table sizes, the library's own; a table resized
+    // to another size runs the in-line kernels)
+    const auto p2 = [](long long n) { return n > 0 && (n & (n - 1)) == 0; };
+    bool fused = h->fused && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0 && p2(h->t.capacity) &&
+                 p2(h->t.shard_cap);
     if (fused && (flags & TSDF_DEVICE_PTRS))
         fused = (uintptr_t)depth % (dk == TSDF_DEPTH_U16_MM ? 8 : 16) == 0 && (uintptr_t)color % 4 == 0 &&
                 ((size_t)H * W) % 4 == 0;
@@ -977,7 +989,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
     if (!h) return TSDF_OK;
     (void)hipSetDevice(h->b.device);
     h->b.release();
-    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list};
+    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (h->vmm) {
