@@ -98,8 +98,8 @@ int tsdf_device_count(int* n);
 int tsdf_dense_create(const int64_t dims[3], const int64_t index_offset[3], const float origin[3],
                       double voxel_size, double trunc, int device, tsdf_dense_t** out);
 /* Cyclic brick-column shard of a volume of global_dims voxels: shard s of n owns
- * the 8-voxel x-columns c with c % n == s, stored contiguously in local x order, so every rank
- * sees a similar share of each frame's frustum.  The shard's local dims are
+ * the 8-voxel x-columns c with c % 2n in {s, 2n-1-s} (mirrored pairs), stored contiguously in
+ * local x order, so every rank sees a similar share of each frame's frustum.  The shard's local dims are
  * (sum of its column widths, Y, Z); tsdf_dense_get/set use that local C-order.  n_shards = 1
  * is tsdf_dense_create with a zero offset.  Replaces the same constructor as above. */
 int tsdf_dense_create_shard(const int64_t global_dims[3], int shard, int n_shards,

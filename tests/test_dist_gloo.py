@@ -183,6 +183,19 @@ def test_cyclic_columns_partition():
             allx = np.sort(np.concatenate(cols))
             assert np.array_equal(allx, np.arange(nx))
             assert max(len(c) for c in cols) - min(len(c) for c in cols) <= 8
+            assert all((np.diff(c) > 0).all() for c in cols)  # local rows in global x order
+
+
+def test_cyclic_columns_mirrored_pairs_even_out_an_x_ramp():
+    """Shard s owns columns s and 2N-1-s of every 2N (tsdf_dense_create_shard): a work density
+    linear in x gives every rank the same total over whole periods (plain c % N == s gave rank
+    0 the lightest column of every period)."""
+    from tsdf_amd import sharding
+    for world in (2, 4, 8):
+        nx = 512
+        tot = [sharding.columns(r, world, nx).sum() for r in range(world)]
+        assert len(set(tot)) == 1
+        assert list(sharding.columns(1, world, nx)[8:16] // 8) == [2 * world - 2] * 8
 
 
 def test_hash_owner_matches_oracle_keys():

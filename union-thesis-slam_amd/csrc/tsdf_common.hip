@@ -136,7 +136,7 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     vol.vs = vs;
     vol.trunc = trunc;
     vol.rtrunc = 1.0 / trunc;  // IEEE division: RN(1/trunc)
-    vol.xstride = kBrickEdge;
+    vol.xstride = vol.xodd = kBrickEdge;
     vol.sb[0] = vol.sb[1] = vol.sb[2] = 2;  // 4x4x4-brick superbricks
     vol.shard = 0;
     vol.n_shards = 1;

@@ -33,8 +33,10 @@ enum Stat { ST_VOXELS = 0, ST_VISITED, ST_TOUCHED, ST_ALLOC, ST_PROBE, ST_LOOKUP
 struct Vol {
     int dims[3];    // voxels of this shard
     int off[3];     // global voxel index of local (0,0,0)
-    int xstride;    // global x distance between consecutive local brick columns (8: contiguous;
-                    // 8*S: cyclic brick-column sharding over S ranks)
+    int xstride;    // global x distance between local brick columns 2k and 2k+2 is 2*xstride (8:
+                    // contiguous; 8*S: brick-column sharding over S ranks)
+    int xodd;       // global x distance from local column 2k to 2k+1 (8: contiguous; xstride:
+                    // plain cyclic; 8*(2S-1-2s): the mirrored pairs s, 2S-1-s of shard s)
     int sb[3];      // log2 superbrick edge in bricks per axis (sum 6: one wave = 64 bricks)
     int nb[3];      // bricks per axis (ceil(dims/8))
     int shard, n_shards;
@@ -43,6 +45,11 @@ struct Vol {
     double rtrunc;  // RN(1 / trunc), from the host's IEEE division (Markstein quotient, below)
     const double* rcp;  // kRcpBig entries RN(1/n) in HBM (the first kRcpTab copied to LDS)
 };
+
+// Global x of local brick column c's first voxel, less off[0].
+__host__ __device__ inline int col_gx(const Vol& v, int c) {
+    return (c >> 1) * 2 * v.xstride + (c & 1) * v.xodd;
+}
 
 // Per-frame constants (by value).
 struct Frame {
@@ -229,8 +236,8 @@ __device__ inline BrickBox brick_box(const Vol& v, const double* eye, int bx, in
         const int lo = bb[a] * kBrickEdge;
         const int hi = min(lo + nn[a] * kBrickEdge - 1, v.dims[a] - 1);
         // global indices of the low / high corner (x: local brick column -> global column)
-        const int glo = (a == 0) ? bb[0] * v.xstride : lo;
-        const int ghi = (a == 0) ? (hi >> 3) * v.xstride + (hi & 7) : hi;
+        const int glo = (a == 0) ? col_gx(v, bb[0]) : lo;
+        const int ghi = (a == 0) ? col_gx(v, hi >> 3) + (hi & 7) : hi;
         r.p0[a] = (double)v.origin[a] + v.vs * (double)(glo + v.off[a]);
         r.ext[a] = (float)(v.vs * (double)(ghi - glo));
         r.ctr[a] = (float)(r.p0[a] + 0.5 * v.vs * (double)(ghi - glo) - eye[a]);
@@ -632,7 +639,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const bool col_in = lx < v.dims[0] && ly < v.dims[1];
     const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge) - zoff;  // valid steps of this part
     // vox2world (grid_fusion.py:170-181); lanes 0..7 compute the brick's 8 z coordinates
-    const double px = vox_world(v.origin[0], v.vs, v.off[0] + bx * v.xstride + (lane >> 3));
+    const double px = vox_world(v.origin[0], v.vs, v.off[0] + col_gx(v, bx) + (lane >> 3));
     const double py = vox_world(v.origin[1], v.vs, v.off[1] + ly);
     const double pz_l = vox_world(v.origin[2], v.vs, v.off[2] + bz * kBrickEdge + (lane & 7));  // lane k: z = k
     // z-part waves (NZ = 4, dense): this part's z coordinates read out of the lanes once per item

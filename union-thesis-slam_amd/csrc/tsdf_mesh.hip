@@ -289,7 +289,7 @@ void Mesh::release() {
 
 int mesh_domain(const Vol& v, long long global_x, const int64_t* halo_gx, long long n_halo, MeshDomain* d) {
     const int nl = v.dims[0];
-    auto gx_of = [&](int lr) { return v.off[0] + (lr >> 3) * v.xstride + (lr & 7); };
+    auto gx_of = [&](int lr) { return v.off[0] + col_gx(v, lr >> 3) + (lr & 7); };
     if (global_x > 0) {
         d->xlo = 0;
         d->xhi = (int)global_x;
@@ -337,7 +337,7 @@ int mesh_halo_rows(const Vol& v, long long global_x, std::vector<long long>* out
     if (global_x <= 0 || global_x > (1 << 24)) return set_error(TSDF_E_ARG, "bad global x extent %lld", global_x);
     std::vector<char> local((size_t)global_x, 0);
     for (int lr = 0; lr < v.dims[0]; ++lr) {
-        const long long gx = v.off[0] + (long long)(lr >> 3) * v.xstride + (lr & 7);
+        const long long gx = v.off[0] + (long long)col_gx(v, lr >> 3) + (lr & 7);
         if (gx >= global_x) return set_error(TSDF_E_ARG, "local row at x %lld beyond the global extent", gx);
         local[gx] = 1;
     }

@@ -39,12 +39,14 @@ def slab(rank: int, world: int, nx: int, align: int = BRICK):
 
 def columns(rank: int, world: int, nx: int):
     """Global x indices owned by `rank` under cyclic brick-column sharding (the layout
-    tsdf_dense_create_shard builds): the 8-voxel x-columns c with c % world == rank, in order.
-    Every rank then sees a similar share of each frame's frustum, unlike contiguous slabs."""
+    tsdf_dense_create_shard builds): in every period of 2*world 8-voxel x-columns, columns rank
+    and 2*world-1-rank (mirrored pairs), in order.  Every rank then sees a similar share of each
+    frame's frustum, unlike contiguous slabs, and a work density drifting along x evens out."""
     if not (0 <= rank < world):
         raise ValueError(f"rank {rank} outside world {world}")
     x = np.arange(nx, dtype=np.int64)
-    own = x[(x // BRICK) % world == rank]
+    ph = (x // BRICK) % (2 * world)
+    own = x[(ph == rank) | (ph == 2 * world - 1 - rank)]
     if own.size == 0:
         raise ValueError(f"rank {rank} of {world} owns no 8-voxel column of {nx}")
     return own
