@@ -292,6 +292,9 @@ def main():
         f"kernel {st['kernel_ms']:.1f} ms over {st['kernel_launches']} launches, "
         f"bricks visited/frame {st['bricks_visited'] / Kf:.0f}, touched/frame {st['bricks_touched'] / Kf:.0f}")
     dense_bytes = 3 * 4 * len(vol.x_index) * X * X
+    # side legs that fail are reported in the line's top-level "errors" (every rank's), never
+    # silently: the throughput measurement above stands either way
+    errors = []
     # ---- PCIe-inclusive rate: the same frames from pageable host memory (not `value`) -------
     ingest = None
     if not args.no_ingest:
@@ -324,13 +327,15 @@ def main():
             t0 = time.perf_counter()
             sharding.integrate_broadcast(vol, K, dh, ch, Tinv[:ni] if rank == 0 else None)
             tb = max_over_ranks(time.perf_counter() - t0)
-            bcast = {"frames_per_s": round(ni / tb, 1), "frames": ni,
-                     "source": "rank 0's host frames, pinned H2D once, broadcast to every rank in chunks "
-                               "of 64 over RCCL (sharding.integrate_broadcast), integrated while the next "
-                               "chunk travels"}
+            be = dist.get_backend()
+            bcast = {"frames_per_s": round(ni / tb, 1), "frames": ni, "backend": be,
+                     "source": f"rank 0's host frames, pinned H2D once, broadcast to every rank in chunks "
+                               f"of 64 over {'RCCL' if be == 'nccl' else be} in {sharding._device().type} "
+                               f"buffers (sharding.integrate_broadcast), integrated while the next chunk travels"}
             log(f"[rank {rank}] broadcast ingest: {ni / tb:.0f} frames/s")
-        except Exception as e:  # reported, never fatal to the throughput measurement
+        except Exception as e:  # reported (top-level "errors"), never fatal to the throughput measurement
             bcast = {"error": f"{type(e).__name__}: {e}"[:300]}
+            errors.append(f"broadcast_ingest, rank {rank}: " + bcast["error"])
             log(f"[rank {rank}] broadcast ingest failed: {e}")
     # ---- mesh extraction of the fused volume (not part of `value`) ----
     mesh = None
@@ -350,8 +355,9 @@ def main():
                     "note": "per-shard marching cubes with the neighbours' border rows (point-to-point "
                             "exchange + extraction, max over ranks); the union is the unsharded mesh"}
             log(f"[rank {rank}] sharded mesh: {len(part[1])} triangles in {tm * 1e3:.1f} ms")
-        except Exception as e:  # reported, never fatal to the throughput measurement
+        except Exception as e:  # reported (top-level "errors"), never fatal to the throughput measurement
             mesh = {"error": f"{type(e).__name__}: {e}"[:300]}
+            errors.append(f"sharded mesh, rank {rank}: " + mesh["error"])
             log(f"[rank {rank}] sharded mesh failed: {e}")
     if not args.no_mesh and rank == 0 and n == 1:
         import ctypes
@@ -385,7 +391,7 @@ def main():
         hdt_max = max_over_ranks(hdt)
         hvox = sum_over_ranks(float(hs["voxel_updates"]))
         used = sum_over_ranks(info["used"])
-        hash_bytes = info["capacity"] * (8 + 4) + info["pool_capacity"] * (3 * 4 * 512 + 64 + 4)
+        hash_bytes = info["slots"] * (8 + 4) + info["pool_capacity"] * (3 * 4 * 512 + 64 + 4)
         hash_res = {"frames_per_s": round(Kf / hdt_max, 1),
                     "mvox_updates_per_s": round(hvox / hdt_max / 1e6, 1),
                     "ms_per_step": round(1e3 * hdt_max / Ks, 4),
@@ -496,6 +502,12 @@ def main():
         cpu = cpu_baseline(dh, ch, poses[f0], K, f0)
         log(f"[rank 0] cpu baseline: {cpu['value']} frames/s ({time.perf_counter() - t0:.1f} s)")
 
+    if n > 1:  # every rank's side-leg failures, on rank 0
+        every = [None] * n
+        dist.all_gather_object(every, errors)
+        errors = [e for part in every for e in part]
+    if errors:
+        log("SIDE-LEG ERRORS: " + " | ".join(errors))
     if rank == 0:
         line = {
             "metric": "depth frames/sec (640x480 into 512^3 @ 2 cm dense TSDF; hash alongside)",
@@ -516,6 +528,7 @@ def main():
             "mesh": mesh,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "errors": errors,
         }
         print(json.dumps(line), flush=True)
     if n > 1:

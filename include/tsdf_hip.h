@@ -77,7 +77,8 @@ typedef struct {
 } tsdf_stats_t;
 
 typedef struct {
-    int64_t capacity;         /* slots in the open-addressed block table (the "buckets") */
+    int64_t capacity;         /* the table size of the API (map_size: hash_function's modulus, doubled
+                                 by double_table_size and the 0.75 load-factor policy) */
     int64_t used;             /* live block keys */
     int64_t tombstones;       /* removed keys not yet reclaimed by a rehash */
     int64_t displaced;        /* live keys not in their home slot ("collisions") */
@@ -85,6 +86,7 @@ typedef struct {
     int64_t blocks_in_pool;   /* blocks handed out by the pool (live + free list) */
     int64_t pool_capacity;    /* blocks the pool can hold before it must grow */
     int64_t entries;          /* voxel entries (occupancy bits set), = count_num_hash_entries */
+    int64_t slots;            /* slots of the open-addressed device table: the power of two >= capacity */
 } tsdf_hash_info_t;
 
 const char* tsdf_last_error(void);
@@ -170,11 +172,13 @@ int tsdf_dense_stats(tsdf_dense_t* h, tsdf_stats_t* out, int reset);
 int tsdf_dense_set_profiling(tsdf_dense_t* h, int on);
 
 /* ---- voxel hash: replaces HashTable (hash_fusion.py:29-507) --------------------------------
- * Keys are 8x8x8 voxel blocks; the home slot of block (bx,by,bz) is the reference's
- * hash_function (hash_fusion.py:182-190) of the block coordinates, floor-mod `capacity`, in
- * int64 (int_bits = 64, NumPy 2 / Linux) or wrapping int32 (int_bits = 32, the author's
- * Windows run).  Open addressing, linear probe, lock-free CAS insert.  Shard s of n_shards
- * owns the blocks whose home slot falls in [s*capacity/n, (s+1)*capacity/n). */
+ * Keys are 8x8x8 voxel blocks.  `capacity` is the reference's map_size (hash_fusion.py:34): the
+ * modulus of hash_function (hash_fusion.py:182-190, tsdf_hash_keys) and the size the 0.75
+ * load-factor policy is kept against.  The device table has S = the power of two >= capacity
+ * slots; the home slot of block (bx,by,bz) is the reference's hash of the block coordinates in
+ * int64 (int_bits = 64, NumPy 2 / Linux) or wrapping int32 (int_bits = 32, the author's Windows
+ * run), floor-mod S.  Open addressing, linear probe, lock-free CAS insert.  Shard s of n_shards
+ * owns the blocks whose home slot (in the S of create) falls in [s*S/n, (s+1)*S/n). */
 int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_size,
                      double trunc, int64_t capacity, int64_t max_blocks, int int_bits,
                      int shard, int n_shards, int device, tsdf_hash_t** out);
@@ -203,7 +207,8 @@ int tsdf_hash_lookup(tsdf_hash_t* h, const int64_t* ijk, int64_t n, float* tsdf,
 int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float* tsdf,
                      const float* weight, const float* color, int64_t* slot, int32_t* local);
 int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* removed);
-/* double_table_size (hash_fusion.py:414-437): rehash every live key into 2x the slots. */
+/* double_table_size (hash_fusion.py:414-437): the table size becomes new_capacity (the device
+ * table rehashes into the power of two >= it when that changes). */
 int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity);
 int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out);
 /* Sparse block transfer for merging bucket-range shards: only live blocks move.

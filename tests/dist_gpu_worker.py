@@ -6,7 +6,8 @@ bucket-range hash shard integrate the same frames, then
   * sharding.gather_meshes / gather_volume -- the union on rank 0;
   * sharding.merge_hash_shards -- live blocks only, imported into one table on rank 0.
 Rank 0 saves the results to <out>/dist.npz for the parent test to compare with one unsharded
-volume."""
+volume.  With the "cuda" argument every collective buffer is a device tensor (the branches an
+RCCL run takes), moved by gloo."""
 import contextlib
 import io
 import os
@@ -23,12 +24,14 @@ for p in (os.path.join(REPO, "union-thesis-slam_amd"), os.path.join(REPO, "oracl
 C1 = [[-2.56, 2.56], [-2.56, 2.56], [0.0, 5.12]]
 
 
-def main(out):
+def main(out, buffers="host"):
     import torch.distributed as dist
     from conftest import load_lounge, lounge_intrinsics
     from tsdf_amd import grid_fusion, hash_fusion, sharding
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
+    # "cuda": the collective buffers in device memory, as under RCCL (sharding.set_buffer_device)
+    sharding.set_buffer_device("cuda" if buffers == "cuda" else None)
     K = lounge_intrinsics()
     with contextlib.redirect_stdout(io.StringIO()):
         vol = grid_fusion.TSDFVolume(np.array(C1), 0.04, shard=(rank, world))
@@ -65,10 +68,11 @@ def main(out):
         np.savez(os.path.join(out, "dist.npz"), v=mesh[0], f=mesh[1], n=mesh[2], c=mesh[3],
                  t=state[0], w=state[1], col=state[2], ht=ht_t, hw=ht_w, hc=ht_c,
                  merged_used=merged.info()["used"], shard_blocks=tot["blocks"],
-                 part_verts=len(part[0]), bcast_ok=tot["bcast_ok"])
+                 part_verts=len(part[0]), bcast_ok=tot["bcast_ok"],
+                 dev=int(sharding._device().type == "cuda"))
     dist.barrier()
     dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "host")

@@ -123,3 +123,88 @@ def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe, vmm):
     g.integrate_batch(d, c, K, Tinv)
     for a, b in zip(g.get_state(), h.get_state()):
         assert np.array_equal(a, b)
+
+
+def test_deferred_hash_restage_after_a_pending_overflow():
+    """Round-2 advisor finding: a per-frame call that fills a batch launches it and leaves its
+    overflow check (grow, exact re-run of the skipped bricks) to the next call; that re-run reads
+    the batch's staging slots.  A power-of-two table (the fused launch, which defers the check)
+    with the smallest pool overflows in the first batch; the next frame is larger, so the staging
+    slots are reallocated -- the pending re-run must happen first.  Equal to the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    d, c, poses = _synth(12, start=420)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Kh = K.copy()
+    Kh[:2] /= 2.0
+    Kh[0, 2] -= 0.25  # pixel (u, v) of the half image is pixel (2u + 0.5, 2v + 0.5) of the full one
+    Kh[1, 2] -= 0.25
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.08, defer=False)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.08, 1 << 6, max_blocks=64)
+    for f in range(12):
+        half = f < 8  # a full deferred batch of 320x240 frames, then 640x480
+        m = (d[f, ::2, ::2] if half else d[f]).astype(float) / 1000.0
+        col = np.ascontiguousarray(c[f, ::2, ::2] if half else c[f])
+        Kf = Kh if half else K
+        g.integrate(col, np.ascontiguousarray(m), Kf, poses[f])
+        h.integrate(col, np.ascontiguousarray(m), Kf, poses[f])
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+    assert h.stats()["bricks_skipped"] > 0  # the deferred overflow re-run did run
+    assert h.info()["pool_capacity"] > 64
+
+
+@pytest.mark.parametrize("map_size", [1000, 1000000, 2000000])
+def test_reference_table_sizes_take_the_fused_launch(map_size):
+    """HashTable(map_size=10^6) (the reference default, hash_fusion.py:34) and 2*10^6
+    (hash_demo1.py:110): the device table is the next power of two, so they run the fused z-half
+    launch; hash_function keeps the reference's modulus; results equal the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    d, c, poses = _synth(16, start=250)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.04, map_size)
+    info = h.info()
+    assert info["capacity"] == map_size and info["slots"] == 1 << (map_size - 1).bit_length()
+    xyz = np.array([[3, 1000, -7], [123456, 5, 99]], np.int64)
+    for p in xyz:
+        ref = ((int(p[0]) * 73856093) ^ (int(p[1]) * 19349669) ^ (int(p[2]) * 83492791)) % map_size
+        assert h.hash_function(p) == ref
+    h.set_profiling(True)
+    h.integrate_batch(d, c, K, Tinv)
+    st = h.stats()
+    assert st["bricks_skipped"] == 0 or map_size == 1000
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.04)
+    g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+    info = h.info()
+    assert info["used"] < 0.75 * info["capacity"] + 1 and info["slots"] >= info["capacity"]
+
+
+def test_f64_device_frames_match_the_u16_encoding():
+    """f64-metre frames from device pointers (the drop-in's depth kind on the fused k_fused<DK=1>
+    and k_fused_hash<1> launches) against the u16 millimetres of the same frames: f64(mm)/1000 is
+    exactly the u16 path's conversion, so dense and hash states are bit-identical."""
+    import torch
+    from tsdf_amd import _ffi, grid_fusion, hash_fusion
+    d, c, poses = _synth(13, start=520)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    d64 = torch.from_numpy(d.astype(np.float64) / 1000.0).cuda()
+    d16 = torch.from_numpy(np.ascontiguousarray(d).view(np.int16)).cuda()
+    cc = torch.from_numpy(c).cuda()
+    torch.cuda.synchronize()
+    outs = []
+    for dd, kind in ((d64, _ffi.DEPTH_F64_M), (d16, _ffi.DEPTH_U16_MM)):
+        g = grid_fusion.TSDFVolume(np.array(BNDS), 0.04)
+        g.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True,
+                          depth_kind=kind)
+        h = hash_fusion.HashTable(np.array(BNDS), 0.04, 1 << 14)
+        h.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True,
+                          depth_kind=kind)
+        outs.append((g.get_state(), h.get_state()))
+    (g64, h64), (g16, h16) = outs
+    for a, b, x in zip(g64, g16, h64):
+        assert _same(a, b) and _same(x, b)
+    for a, b in zip(h16, g16):
+        assert _same(a, b)

@@ -54,6 +54,37 @@ KERNEL(k_add_f32, float, BODY8("v_add_f32", float, "v"))
 KERNEL(k_rcp_f32, float, BODY8_1("v_rcp_f32"))
 KERNEL(k_rndne_f32, float, BODY8_1("v_rndne_f32"))
 KERNEL(k_pk_fma_f32, double, BODY8_3("v_pk_fma_f32"))
+// conversions: 8 independent results per iteration from a source of the other width
+#define BODYX(INS, SRC)                                                                          \
+    asm volatile(INS " %0, %8\n" INS " %1, %8\n" INS " %2, %8\n" INS " %3, %8\n" INS " %4, %8\n"  \
+                 INS " %5, %8\n" INS " %6, %8\n" INS " %7, %8\n"                                  \
+                 : "=v"(a[0]), "=v"(a[1]), "=v"(a[2]), "=v"(a[3]), "=v"(a[4]), "=v"(a[5]),      \
+                   "=v"(a[6]), "=v"(a[7])                                                      \
+                 : "v"(SRC))
+#define KERNELX(NAME, T, S, INS)                                                                \
+    __global__ void NAME(T* out, long long* cyc, T b0) {                                        \
+        T a[8];                                                                                 \
+        S src = (S)(threadIdx.x + 1);                                                           \
+        __syncthreads();                                                                        \
+        const long long t0 = __builtin_amdgcn_s_memtime();                                      \
+        for (int it = 0; it < kIters; ++it) {                                                   \
+            BODYX(INS, src);                                                                    \
+            asm volatile("" : "+v"(src));                                                       \
+        }                                                                                       \
+        const long long t1 = __builtin_amdgcn_s_memtime();                                      \
+        T s = 0;                                                                                \
+        for (int i = 0; i < 8; ++i) s += a[i];                                                  \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = s + b0;                                    \
+        if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0; \
+    }
+KERNEL(k_mov_b64, double, BODY8_1("v_mov_b64"))
+KERNELX(k_cvt_f64_f32, double, float, "v_cvt_f64_f32")
+KERNELX(k_cvt_f32_f64, float, double, "v_cvt_f32_f64")
+KERNELX(k_cvt_f64_u32, double, unsigned, "v_cvt_f64_u32")
+KERNELX(k_cvt_i32_f64, float, double, "v_cvt_i32_f64")
+KERNEL(k_cvt_u32_f32, float, BODY8_1("v_cvt_u32_f32"))
+KERNEL(k_cvt_ubyte1, float, BODY8_1("v_cvt_f32_ubyte1"))
+KERNEL(k_mad_u24, float, BODY8_3("v_mad_u32_u24"))
 KERNEL(k_pk_mul_f32, double, BODY8("v_pk_mul_f32", double, "v"))
 
 typedef void (*kd)(double*, long long*, double);
@@ -81,7 +112,28 @@ void run(const char* name, K k, int waves_per_simd) {
     hipFree(cyc);
 }
 
+// v_cvt_pk_u8_f32 rounding: every quarter value in [-2, 260] against rint + clamp
+__global__ void k_pk_u8(unsigned* bad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const float x = -2.0f + 0.25f * (float)i;
+    if (x > 260.0f) return;
+    unsigned r;
+    asm volatile("v_cvt_pk_u8_f32 %0, %1, 0, 0" : "=v"(r) : "v"(x));
+    const float e = fminf(fmaxf(rintf(x), 0.0f), 255.0f);
+    if ((r & 0xFF) != (unsigned)e) atomicAdd(bad, 1u);
+}
+
 int main() {
+    {
+        unsigned* bad;
+        hipMalloc(&bad, 4);
+        hipMemset(bad, 0, 4);
+        hipLaunchKernelGGL(k_pk_u8, dim3(8), dim3(256), 0, 0, bad);
+        unsigned h = 0;
+        hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost);
+        printf("v_cvt_pk_u8_f32 vs rint+clamp: %u mismatches of 1049 quarter values\n", h);
+        hipFree(bad);
+    }
     for (int w : {1, 4}) {
         run<double>("v_fma_f64", (kd)k_fma_f64, w);
         run<double>("v_add_f64", (kd)k_add_f64, w);
@@ -96,6 +148,14 @@ int main() {
         run<float>("v_rndne_f32", (kf)k_rndne_f32, w);
         run<double>("v_pk_fma_f32", (kd)k_pk_fma_f32, w);
         run<double>("v_pk_mul_f32", (kd)k_pk_mul_f32, w);
+        run<double>("v_mov_b64", (kd)k_mov_b64, w);
+        run<double>("v_cvt_f64_f32", (kd)k_cvt_f64_f32, w);
+        run<float>("v_cvt_f32_f64", (kf)k_cvt_f32_f64, w);
+        run<double>("v_cvt_f64_u32", (kd)k_cvt_f64_u32, w);
+        run<float>("v_cvt_i32_f64", (kf)k_cvt_i32_f64, w);
+        run<float>("v_cvt_u32_f32", (kf)k_cvt_u32_f32, w);
+        run<float>("v_cvt_f32_ubyte1", (kf)k_cvt_ubyte1, w);
+        run<float>("v_mad_u32_u24", (kf)k_mad_u24, w);
     }
     return 0;
 }

@@ -2,9 +2,12 @@
 """Predict the N-GPU strong-scaling curve of the dense bench on ONE GPU: every rank's shard of
 512^3 @ 2 cm is built and timed in turn on the same synthetic frames; the N-rank job time is the
 max over its ranks (ranks never exchange data while integrating).  Compares contiguous slabs
-with cyclic 8-voxel column shards.
+with cyclic 8-voxel column shards.  --hash: the voxel hash's bucket-range shards
+(BASELINE config[4]: 2^22 buckets; --extent 1024 puts the same room into a 1024^3 @ 1 cm extent),
+with each rank's frames/s, Mvoxel-updates/s and HBM state bytes.
 
   python tools/scaling_sim.py [--steps 800] [--warmup 48] [--worlds 1,2,4,8]
+  python tools/scaling_sim.py --hash [--extent 512|1024] [--only 8:5]
 """
 import argparse
 import contextlib
@@ -26,6 +29,8 @@ def main():
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--only", default=None, help="W:R -- time only rank R of world W (for profiling)")
+    ap.add_argument("--hash", action="store_true", help="bucket-range hash shards instead of dense columns")
+    ap.add_argument("--extent", type=int, default=512, help="hash: 512 (2 cm) or 1024 (1 cm) voxels per axis")
     a = ap.parse_args()
     import torch
     from tsdf_amd import grid_fusion, scene, sharding
@@ -60,6 +65,8 @@ def main():
         return time.perf_counter() - t0
 
     out = {}
+    if a.hash:
+        return hash_shards(a, timed, bnds)
     if a.only:
         world, r = (int(x) for x in a.only.split(":"))
         with contextlib.redirect_stdout(sys.stderr):
@@ -93,6 +100,48 @@ def main():
     for k, v in out.items():
         n = int(k.lstrip("slabcyclic"))
         v["predicted_efficiency"] = round(v["fps"] / (n * base), 3)
+    print(json.dumps(out))
+
+
+def hash_shards(a, timed, bnds):
+    """Bucket-range shards of the voxel hash (shard r of N owns the blocks whose home slot is in
+    [r S / N, (r+1) S / N), S = 2^22): each rank's shard timed in turn on the same frames."""
+    import torch
+    from tsdf_amd import hash_fusion
+    vs = 10.24 / a.extent
+    per_block = 3 * 4 * 512 + 64 + 4
+    out = {"extent": f"{a.extent}^3 @ {vs * 100:g} cm", "buckets": 1 << 22,
+           "dense_shard_bytes_note": "dense grid of the same extent / N: 12 B per voxel"}
+    worlds = [int(a.only.split(":")[0])] if a.only else [int(w) for w in a.worlds.split(",")]
+    for world in worlds:
+        ranks = [int(a.only.split(":")[1])] if a.only else range(world)
+        res = []
+        for r in ranks:
+            with contextlib.redirect_stdout(sys.stderr):
+                ht = hash_fusion.HashTable(bnds.copy(), vs, 1 << 22, shard=r, n_shards=world,
+                                           max_blocks=1 << 15)
+            timed(ht, 0, a.warmup)
+            ht.stats(reset=True)
+            t = timed(ht, a.warmup, a.steps)
+            st, info = ht.stats(), ht.info()
+            state = info["slots"] * 12 + info["pool_capacity"] * per_block
+            res.append({"rank": r, "fps": round(a.steps / t, 1),
+                        "mvox_updates_per_s": round(st["voxel_updates"] / t / 1e6, 1),
+                        "blocks_live": info["used"], "pool_capacity": info["pool_capacity"],
+                        "hbm_state_bytes": state,
+                        "dense_shard_bytes": 12 * a.extent ** 3 // world,
+                        "bricks_skipped": st["bricks_skipped"]})
+            print(json.dumps(res[-1]), file=sys.stderr, flush=True)
+            ht.close()
+            del ht
+            torch.cuda.empty_cache()
+        t_max = min(x["fps"] for x in res)
+        out[f"hash{world}"] = {"fps": t_max, "ranks": res}
+    if "hash1" in out:
+        base = out["hash1"]["fps"]
+        for k, v in out.items():
+            if k.startswith("hash"):
+                v["predicted_efficiency"] = round(v["fps"] / (int(k[4:]) * base), 3)
     print(json.dumps(out))
 
 

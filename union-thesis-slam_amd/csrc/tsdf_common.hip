@@ -108,6 +108,17 @@ __global__ void k_zero_u64(unsigned long long* p, int n) {
 }
 
 namespace {
+// Vol::canon check over the first n voxels of the brick pool: weights integers >= 0, colours
+// canonical (the state integrate writes); any other value clears the flag (k_set / import).
+__global__ void k_check_canon(const float* __restrict__ w, const float* __restrict__ c, size_t n, int* bad) {
+    bool ok = true;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float wi = w[i], ci = c[i];
+        ok = ok && wi >= 0.0f && wi == truncf(wi) && ci >= 0.0f && ci < 16777216.0f && ci == truncf(ci);
+    }
+    if (__ballot(!ok) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
 __global__ void k_fill_rcp(double* r) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < kRcpBig) r[i] = 1.0 / (double)i;  // IEEE division: RN(1/i) (r[0] = inf, unused)
@@ -140,6 +151,7 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     vol.sb[0] = vol.sb[1] = vol.sb[2] = 2;  // 4x4x4-brick superbricks
     vol.shard = 0;
     vol.n_shards = 1;
+    vol.canon = 1;  // a fresh state (1, 0, 0) everywhere
     n_bricks = (long long)vol.nb[0] * vol.nb[1] * vol.nb[2];
     if (n_bricks >= (1ll << 24)) return set_error(TSDF_E_ARG, "too many bricks (%lld >= 2^24)", n_bricks);
     TSDF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -391,7 +403,25 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->fy = (double)(float)K[4];
         fr->cx = (double)(float)K[2];
         fr->cy = (double)(float)K[5];
-        fr->half_m = 0.5 - frame_margin(W, H, fr->cx, fr->cy);
+        const double margin = frame_margin(W, H, fr->cx, fr->cy);
+        fr->half_m = 0.5 - margin;
+        for (int j = 0; j < 4; ++j) {
+            fr->Tf[j] = T[j] * fr->fx;
+            fr->Tf[4 + j] = T[4 + j] * fr->fy;
+        }
+        {  // the fast path's depth limit (fold_bound) as the high dword of a positive f64, rounded up
+            double wmax[3];
+            for (int a = 0; a < 3; ++a) {
+                const long long gmax = (a == 0 ? (long long)vol.off[0] + col_gx(vol, vol.nb[0] - 1) + kBrickEdge
+                                               : (long long)vol.off[a] + vol.dims[a]);
+                wmax[a] = fabs((double)vol.origin[a]) + vol.vs * (double)gmax + 1.0;
+            }
+            const double zmin = fold_bound(T, fr->fx, fr->fy, wmax, margin);
+            long long bits;
+            std::memcpy(&bits, &zmin, sizeof bits);
+            const long long hi = (std::isfinite(zmin) && zmin < 1e300) ? (bits >> 32) + 1 : 0x7FEFFFFFll;
+            fr->zmin_hi = (int)std::min<long long>(hi, 0x7FEFFFFFll);
+        }
         fr->ow = ow ? ow[first + i] : ow_default;
         fr->ow32 = (float)fr->ow;
         fr->H = H;
@@ -509,6 +539,25 @@ unsigned Base::grid_for(const void* kernel, int wg) {
     const long long need = (n_bricks + (wg / 64) - 1) / (wg / 64);
     if (g > need) g = need;
     return (unsigned)(g < 1 ? 1 : g);
+}
+
+int Base::check_canon(long long n_vox) {
+    int* d = nullptr;
+    int bad = 0;
+    TSDF_HIP(hipMalloc(&d, sizeof(int)));
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(int), stream);
+    if (e == hipSuccess && n_vox > 0) {
+        const long long want = (n_vox + 255) / 256;
+        hipLaunchKernelGGL(k_check_canon, dim3((unsigned)std::min<long long>(want, (long long)n_cu * 16)), dim3(256),
+                           0, stream, pool.weight, pool.color, (size_t)n_vox, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, d, sizeof(int), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(d);
+    TSDF_HIP(e);
+    vol.canon = bad ? 0 : 1;
+    return TSDF_OK;
 }
 
 int Base::read_stats(tsdf_stats_t* out, int reset) {

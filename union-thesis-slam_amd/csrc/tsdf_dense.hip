@@ -186,6 +186,7 @@ int dense_run(tsdf_dense* h, int n_frames, const void* depth, int dk, const void
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
+    B.note_frames(ck, ow, n_frames, 1.0);
     // the fused pipeline needs the vectorised prep: u16 or f64 depth + RGB8, W % 4 == 0 and
     // (device frames) 8-byte u16 / 16-byte f64 depth and 4-byte colour alignment of every frame
     // (host frames are staged aligned)
@@ -363,6 +364,7 @@ int tsdf_dense_reset(tsdf_dense_t* h) {
     TSDF_HIP(hipMemsetAsync(B.stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, B.stream));
     TSDF_HIP(hipStreamSynchronize(B.stream));
     B.frames = 0;
+    B.vol.canon = 1;
     return TSDF_OK;
 }
 
@@ -406,7 +408,9 @@ int tsdf_dense_get(tsdf_dense_t* h, float* tsdf_, float* weight_, float* color_)
 
 int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf_, const float* weight_, const float* color_) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
-    return dense_xfer(h, (float*)tsdf_, (float*)weight_, (float*)color_, false);
+    TSDF_TRY(dense_xfer(h, (float*)tsdf_, (float*)weight_, (float*)color_, false));
+    if (weight_ || color_) TSDF_TRY(h->b.check_canon(h->b.n_bricks * kBrickVox));  // Vol::canon
+    return TSDF_OK;
 }
 
 int tsdf_dense_sync(tsdf_dense_t* h) {

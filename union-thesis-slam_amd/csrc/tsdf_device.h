@@ -40,6 +40,9 @@ struct Vol {
     int sb[3];      // log2 superbrick edge in bricks per axis (sum 6: one wave = 64 bricks)
     int nb[3];      // bricks per axis (ceil(dims/8))
     int shard, n_shards;
+    int canon;      // host-tracked: every stored weight is an integer >= 0 and every colour canonical
+                    // (what integrate with obs_weight 1 and RGB8 colour writes); lets the integrate
+                    // skip the per-load integrality checks (a max-range test remains)
     float origin[3];
     double vs, trunc;
     double rtrunc;  // RN(1 / trunc), from the host's IEEE division (Markstein quotient, below)
@@ -57,6 +60,8 @@ struct Frame {
     double fx, fy, cx, cy;    // f64(f32(K))  (cam2pix casts intr to float32, grid_fusion.py:190)
     double ow;                // obs_weight as a Python float (f64)
     double half_m;            // 0.5 - the fast pixel path's boundary margin (frame_margin)
+    double Tf[8];             // the fast pixel path's rows: RN(T[0..3] * fx), RN(T[4..7] * fy)
+    int zmin_hi;              // ... and its depth limit: high dword of zmin (fold_bound, host)
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
     const void* depth;        // depth read by cull/integrate: u16 millimetres or f64 metres
@@ -399,23 +404,39 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 // exhaustively: tools/check_depth_conversion.c) -- one f64 multiply fewer than q = m * 0.001 plus
 // an FMA correction.  depth_raw issues the u16 load; depth_m converts.  For f64 depth (DK == 1)
 // depth_raw is unused and depth_m loads.
-// p is a pixel index < 2^28 (check_frame_args), so byte offsets fit 32 bits: the loads take
-// the SGPR-base + 32-bit VGPR-offset form (no 64-bit address arithmetic per gather)
-template <typename T>
-__device__ inline T texel(const void* base, unsigned p) {
-    return *(const T*)((const char*)base + p * (unsigned)sizeof(T));
+// The per-step gathers go through structured buffer descriptors (stride = texel size, idxen):
+// the hardware scales the pixel index (p < 2^28, check_frame_args), so there is no shift or
+// 64-bit address arithmetic per gather.  num_records = pixels of the image; non-candidate steps
+// read pixel 0.
+__device__ unsigned short buf_ld_u16(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
+                                     int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i16");
+__device__ unsigned buf_ld_u32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
+                               int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
+__device__ double buf_ld_f64(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
+                             int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.f64");
+constexpr int kBufDword3 = 0x00020000;  // gfx9 untyped buffer access
+struct FrameBufs {
+    __amdgpu_buffer_rsrc_t depth, color;
+};
+template <int DK, int CK>
+__device__ inline FrameBufs frame_bufs(const Frame& fr) {
+    const int n = fr.W * fr.H;
+    FrameBufs b;
+    b.depth = __builtin_amdgcn_make_buffer_rsrc((void*)fr.depth, DK == 0 ? 2 : 8, n, kBufDword3);
+    b.color = __builtin_amdgcn_make_buffer_rsrc((void*)(CK == 0 ? (const void*)fr.rgbx : fr.color), 4, n, kBufDword3);
+    return b;
 }
 template <int DK>
-__device__ inline unsigned depth_raw(const Frame& fr, unsigned p) {
-    return DK == 0 ? (unsigned)texel<unsigned short>(fr.depth, p) : 0u;
+__device__ inline unsigned depth_raw(const FrameBufs& fb, unsigned p) {
+    return DK == 0 ? (unsigned)buf_ld_u16(fb.depth, (int)p, 0, 0, 0) : 0u;
 }
 template <int DK>
-__device__ inline double depth_m(const Frame& fr, unsigned p, unsigned raw) {
+__device__ inline double depth_m(const FrameBufs& fb, unsigned p, unsigned raw) {
     if (DK == 0) {  // two-term 1/1000 = C_HI + C_LO: exact for every u16 (tools/check_depth_conversion.c)
         const double m = (double)raw;
         return fma(m, 0.001, m * -2.0858186326137145e-20);
     }
-    return texel<double>(fr.depth, p);
+    return buf_ld_f64(fb.depth, (int)p, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -443,8 +464,14 @@ __device__ inline float div_rn32(float a, float b, float y) {
     return fmaf(r, y, q0);
 }
 
-__device__ inline float2 fma2(float2 a, float2 b, float2 c) {  // v_pk_fma_f32
-    return make_float2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
+// Two f32 lanes per VGPR pair: the packed ALU (v_pk_fma_f32, v_pk_mul_f32, v_pk_add_f32).
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ inline f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ inline f2 rint2(f2 a) { return f2{rintf(a.x), rintf(a.y)}; }
+__device__ inline f2 div_rn32x2(f2 a, f2 b, f2 y) {  // div_rn32 on both lanes
+    const f2 q0 = a * y;
+    const f2 r = pk_fma(-q0, b, a);
+    return pk_fma(r, y, q0);
 }
 
 // The fast path's pixel error is < |u - c| * 2^-24.3 (the bare reciprocal), and wherever the
@@ -454,6 +481,21 @@ __device__ inline float2 fma2(float2 a, float2 b, float2 c) {  // v_pk_fma_f32
 inline double frame_margin(int W, int H, double cx, double cy) {
     const double span = (double)(W > H ? W : H) + fmax(fabs(cx), fabs(cy));
     return fmax(1e-4, 1e-7 * span);
+}
+
+// The fast path folds fx, fy and the translation into its rows: X = fma(Tf2, pz, fma(Tf1, py,
+// fma(Tf0, px, Tf3))) with Tf = RN(T * f) -- four roundings, each within 2^-53 of its operands'
+// magnitudes, so |X - f * x| <= E = 8 * 2^-53 * f * (|T0| X + |T1| Y + |T2| Z + |T3|) for world
+// coordinates bounded by (X, Y, Z) (a factor 2 of slack).  Its pixel error E / z stays below a
+// quarter of the margin where z > zmin = 4 E / margin.  Returns zmin (host).
+inline double fold_bound(const double* T, double fx, double fy, const double wmax[3], double margin) {
+    double e = 0.0;
+    for (int r = 0; r < 2; ++r) {
+        const double* t = T + 4 * r;
+        const double s = fabs(t[0]) * wmax[0] + fabs(t[1]) * wmax[1] + fabs(t[2]) * wmax[2] + fabs(t[3]);
+        e = fmax(e, 8.0 * 0x1p-53 * (r == 0 ? fx : fy) * s);
+    }
+    return 4.0 * e / margin;
 }
 
 // v_cvt_i32_f64 clamps out-of-range inputs to INT_MIN / INT_MAX (a C cast would be undefined
@@ -484,58 +526,58 @@ __device__ inline double readlane_f64(double x, int l) {
 // NZ = 8: one wave per brick (lane = (x, y) column, 8 z-steps).  NZ = 4 (dense only): two waves
 // per brick, one per z-half (zoff = 0 or 4) -- twice the waves for small culled lists (sharded
 // volumes), where one brick per wave leaves SIMDs idle, and half the per-lane registers.
-// 16-byte state halves (4 z-steps each) holding a set bit of `m` (bit k = step k of the part)
-template <int NZ>
-__device__ inline unsigned halves_of(unsigned m) {
-    return NZ == 8 ? (((m & 0x0Fu) ? 1u : 0u) | ((m & 0xF0u) ? 2u : 0u)) : (m ? 1u : 0u);
-}
 
 // Phases 1-3 of one frame for one part (z-steps zoff .. zoff+NZ-1 of a lane's column): project,
-// gather, depth / truncation test.  Returns the valid steps (bit k); fills the packed colour
-// texels and the clamped distances of every step.
+// gather, depth / truncation test.  ok[k]: step k updates its voxel; fills the packed colour
+// texels and the clamped distances of every step.  The per-step conditions stay booleans (lane
+// masks in SGPR pairs): their combinations and wave ballots are scalar instructions, not VALU.
 template <int DK, int CK, int NZ>
-__device__ __forceinline__ unsigned project_part(const Vol& v, const Frame& fr, double px, double py,
-                                                 const double* pzs, double pz_l, int zoff, bool col_in, int nz,
-                                                 unsigned (&cpx)[NZ], double (&dist)[NZ]) {
+__device__ __forceinline__ void project_part(const Vol& v, const Frame& fr, double px, double py,
+                                             const double* pzs, double pz_l, int zoff, bool col_in, int nz,
+                                             unsigned (&cpx)[NZ], double (&dist)[NZ], bool (&ok)[NZ]) {
     constexpr int kPz = NZ < 8 ? NZ : 1;
-    // x/y terms of OpenBLAS's dgemm chain (grid_fusion.py:363-368)
-    const double a0 = fma(fr.T[1], py, fr.T[0] * px);
-    const double a1 = fma(fr.T[5], py, fr.T[4] * px);
+    // the z term of OpenBLAS's dgemm chain (grid_fusion.py:363-368): exact, it feeds the depth test
     const double a2 = fma(fr.T[9], py, fr.T[8] * px);
-    // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the 8 z-steps (no
+    // the pixel's numerators with fx, fy and the translation folded in (fast path only: their
+    // error is bounded on the host, fold_bound, and covered by the boundary margin)
+    const double b0 = fma(fr.Tf[1], py, fma(fr.Tf[0], px, fr.Tf[3]));
+    const double b1 = fma(fr.Tf[5], py, fma(fr.Tf[4], px, fr.Tf[7]));
+    // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the z-steps (no
     // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
     // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
     // the pixel indices leave the f64 domain at once (saturating v_cvt_i32_f64: out-of-range
     // values clamp to INT_MIN / INT_MAX and fail the unsigned bounds test below), which keeps
-    // two f64 per step out of the registers live across the gathers (no VGPR spill left)
+    // two f64 per step out of the registers live across the gathers
     double zc[NZ];
     int iu[NZ], iv[NZ];
-    unsigned inb = 0, slow = 0;
+    bool in[NZ], slow[NZ], any_slow = false;
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
         const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
         const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
-        const double x = fr.T[3] + fma(fr.T[2], pz, a0);
-        const double y = fr.T[7] + fma(fr.T[6], pz, a1);
         const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see frame_margin
-        // one FMA for (x*fx)*rz + cx: within |u - cx| * 2^-24.3 of the reference's
-        // (x*fx)/z + cx, inside the frame_margin boundary margin below
-        const double sx = fma(x * fr.fx, rz, fr.cx), sy = fma(y * fr.fy, rz, fr.cy);
+        // X*rz + cx with X = x*fx up to the folding error: within |u - cx| * 2^-24.3 + E/z of
+        // the reference's (x*fx)/z + cx, inside the frame_margin boundary margin below where
+        // z > zmin (E/z < margin/4; the high-dword integer test is a conservative z > zmin)
+        const double sx = fma(fma(fr.Tf[2], pz, b0), rz, fr.cx), sy = fma(fma(fr.Tf[6], pz, b1), rz, fr.cy);
         const double ux = rint(sx), uy = rint(sy);
         // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
         // but is invalid either way)
-        const bool ok = fabs(sx - ux) < fr.half_m && fabs(sy - uy) < fr.half_m;
-        const bool in = col_in && k < nz && z > 0.0;
+        const bool fine = (fabs(sx - ux) < fr.half_m) & (fabs(sy - uy) < fr.half_m) &
+                          ((int)(__double_as_longlong(z) >> 32) > fr.zmin_hi);
+        in[k] = col_in & (k < nz) & (z > 0.0);
         zc[k] = z;
         iu[k] = cvt_i32_sat(ux);
         iv[k] = cvt_i32_sat(uy);
-        inb |= (unsigned)in << k;
-        slow |= (unsigned)(in && !ok) << k;
+        slow[k] = in[k] & !fine;
+        any_slow |= slow[k];
     }
-    if (__ballot(slow != 0)) {
+    if (__ballot(any_slow)) {
+        const double a0 = fma(fr.T[1], py, fr.T[0] * px);  // the reference's x / y chains
+        const double a1 = fma(fr.T[5], py, fr.T[4] * px);
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            if (!((slow >> k) & 1u)) continue;
+            if (!slow[k]) continue;
             const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
@@ -543,7 +585,7 @@ __device__ __forceinline__ unsigned project_part(const Vol& v, const Frame& fr, 
             iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
         }
     }
-    unsigned cand = 0;
+    bool cand[NZ];
     unsigned pix[NZ];
     const int W = fr.W, H = fr.H;
 #pragma unroll
@@ -551,35 +593,33 @@ __device__ __forceinline__ unsigned project_part(const Vol& v, const Frame& fr, 
         // unsigned bounds on the saturated indices (they come from integral, non-NaN values
         // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
         // np.linalg.inv: all NaN -- fails z > 0)
-        const bool c = ((inb >> k) & 1u) && (unsigned)iu[k] < (unsigned)W && (unsigned)iv[k] < (unsigned)H;
-        cand |= (unsigned)c << k;
-        pix[k] = c ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
+        cand[k] = in[k] & ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
+        pix[k] = cand[k] ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
     }
     // phase 2: gather depth and colour for every step at once, before the depth test, so
-    // all 16 gathers share one memory latency (non-candidates read pixel 0, discarded).  The
+    // all the gathers share one memory latency (non-candidates read pixel 0, discarded).  The
     // scheduling barrier keeps the compiler from sinking each load next to its use, which
-    // under the 128-VGPR budget it otherwise does, serialising the latencies.
+    // under the VGPR budget it otherwise does, serialising the latencies.
+    const FrameBufs fb = frame_bufs<DK, CK>(fr);
     unsigned draw[NZ];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        draw[k] = depth_raw<DK>(fr, pix[k]);
-        cpx[k] = texel<unsigned>(CK == 0 ? (const void*)fr.rgbx : fr.color, pix[k]);
+        draw[k] = depth_raw<DK>(fb, pix[k]);
+        cpx[k] = buf_ld_u32(fb.color, (int)pix[k], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
     double dep[NZ];
 #pragma unroll
-    for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fr, pix[k], draw[k]);
+    for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fb, pix[k], draw[k]);
     // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
-    unsigned vmask = 0;
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
         const double diff = dep[k] - zc[k];
-        const bool ok = ((cand >> k) & 1u) && dep[k] > 0.0 && diff >= -v.trunc;
+        const bool dpos = DK == 0 ? draw[k] != 0u : dep[k] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
+        ok[k] = cand[k] & dpos & (diff >= -v.trunc);
         const double dd = div_rn(diff, v.trunc, v.rtrunc);
         dist[k] = fmin(dd, 1.0);  // np.minimum(1, .) (dd is never NaN)
-        vmask |= (unsigned)ok << k;
     }
-    return vmask;
 }
 
 // Hash z-half waves (NZ = 4, the fused hash launch).  The two halves of a brick are waves 2m and
@@ -618,10 +658,11 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, ListEntry entry, int zoff,
                                        unsigned long long* s_stat, const double* s_rcp,
-                                       int* res = nullptr) {
+                                       unsigned& nupd, int* res = nullptr) {
+    // nupd: the wave's voxel updates, accumulated over its items (scalar popcounts of the step
+    // masks; integrate_list adds it to the statistics once per wave)
     static_assert(NZ == 8 || NZ == 4, "z-parts of 8 or 4 steps");
     constexpr bool kHalfHash = HASH && NZ == 4;  // (requires res)
-    constexpr unsigned kHalves = NZ == 8 ? 3u : 1u;
     const int lane = lane_id();
     const int b = (int)(entry & 0xFFFFFFFFull);
     const unsigned fmask = (unsigned)(entry >> 32);
@@ -679,8 +720,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 if (!((fmask >> fi) & 1u)) continue;
                 unsigned cpx[NZ];
                 double dist[NZ];
-                const unsigned vm = project_part<DK, CK, NZ>(v, bt.f[fi], px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist);
-                need = __ballot(vm != 0) != 0;
+                bool okv[NZ], any = false;
+                project_part<DK, CK, NZ>(v, bt.f[fi], px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist, okv);
+#pragma unroll
+                for (int k = 0; k < NZ; ++k) any |= okv[k];
+                need = __ballot(any) != 0;
             }
             if (!need) return;  // no frame of the batch updates this half
             cur = res_load(rp);
@@ -741,16 +785,19 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         ts[k] = 1.0f;
         cs[k] = 0.0f;
     }
-    // 16-B halves of this lane's column held in registers (bit 0: z 0-3); a half of a block this
-    // launch inserted starts at (1, 0, 0): nothing to load
-    unsigned loaded = (kHalfHash && is_new) ? kHalves : 0u;
-    unsigned dirty = 0;    // halves changed by the batch
+    // 16-B halves of this lane's column held in registers (half h: z 4h .. 4h+3 of the part); a
+    // half of a block this launch inserted starts at (1, 0, 0): nothing to load.  Every half held
+    // is stored at the end (a changed half, or -- a new hash block -- its init).  Lane masks.
+    constexpr int kH = NZ / 4;
+    bool loaded[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) loaded[h] = kHalfHash && is_new;
     unsigned touched = 0;  // voxels updated by any frame of the batch (entry bits, hash)
-    unsigned nupd = 0;  // this lane's voxel updates: one v_bcnt per frame (a per-step count, or a
-                        // wave-level ballot count, costs more VALU)
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
     bool w_table = true;   // ... < kRcpBig
     bool c_canon = true;   // all loaded colours are canonical (canon_color)
+    // the wave-uniform fast-path choices below, refreshed whenever the wave loads state
+    bool fast_t = OW1 && s_rcp, table_t = false, fast_c = CK == 0 && fast_t;
 
 #ifdef TSDF_DIAG
     int d_pairs = 0, d_valid = 0;
@@ -763,8 +810,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #endif
         unsigned cpx[NZ];
         double dist[NZ];
-        const unsigned vmask = project_part<DK, CK, NZ>(v, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist);
-        if (__ballot(vmask != 0) == 0) continue;
+        bool okv[NZ];
+        project_part<DK, CK, NZ>(v, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist, okv);
+        bool need[kH];
+#pragma unroll
+        for (int h = 0; h < kH; ++h) need[h] = okv[4 * h] | okv[4 * h + 1] | okv[4 * h + 2] | okv[4 * h + 3];
+        if (__ballot(need[0] | need[kH - 1]) == 0) continue;
 #ifdef TSDF_DIAG
         ++d_valid;
 #endif
@@ -784,7 +835,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     return;
                 }
                 blk = r;
-                if (is_new) loaded = kHalves;  // a fresh block starts at (1, 0, 0): nothing to load
+                if (is_new) {  // a fresh block starts at (1, 0, 0): nothing to load
+#pragma unroll
+                    for (int h = 0; h < kH; ++h) loaded[h] = true;
+                }
                 if (lane == 0) {
                     atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
                     atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
@@ -795,103 +849,130 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 blk = b;
             }
         }
-        const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
-        // phase 4: state halves not yet in registers, and the colour of every valid voxel
-        const unsigned need = halves_of<NZ>(vmask);
-        const unsigned ld = need & ~loaded;
+        // phase 4: state halves not yet in registers (the wave's first frame that needs them)
+        bool ld[kH];
+        bool any_ld = false;
 #pragma unroll
-        for (int h = 0; h < NZ / 4; ++h) {
-            if (!((ld >> h) & 1u)) continue;
-            const float4 W = *(const float4*)(pool.weight + base + 4 * h);
-            const float4 T = *(const float4*)(pool.tsdf + base + 4 * h);
-            const float4 C = *(const float4*)(pool.color + base + 4 * h);
-            ws[4 * h + 0] = W.x; ws[4 * h + 1] = W.y; ws[4 * h + 2] = W.z; ws[4 * h + 3] = W.w;
-            w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
-            w_table = w_table && table_int(W.x) && table_int(W.y) && table_int(W.z) && table_int(W.w);
-            c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
-            ts[4 * h + 0] = T.x; ts[4 * h + 1] = T.y; ts[4 * h + 2] = T.z; ts[4 * h + 3] = T.w;
-            cs[4 * h + 0] = C.x; cs[4 * h + 1] = C.y; cs[4 * h + 2] = C.z; cs[4 * h + 3] = C.w;
+        for (int h = 0; h < kH; ++h) {
+            ld[h] = need[h] & !loaded[h];
+            any_ld |= ld[h];
         }
-        loaded |= need;
-        dirty |= need;
-        touched |= vmask;
-        nupd += __popc(vmask);
+        if (__ballot(any_ld)) {
+            const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
+#pragma unroll
+            for (int h = 0; h < kH; ++h) {
+                if (!ld[h]) continue;
+                const float4 W = *(const float4*)(pool.weight + base + 4 * h);
+                const float4 T = *(const float4*)(pool.tsdf + base + 4 * h);
+                const float4 C = *(const float4*)(pool.color + base + 4 * h);
+                ws[4 * h + 0] = W.x; ws[4 * h + 1] = W.y; ws[4 * h + 2] = W.z; ws[4 * h + 3] = W.w;
+                if (v.canon) {  // integers >= 0 and canonical colours by construction: a range test
+                    const float wm = fmaxf(fmaxf(W.x, W.y), fmaxf(W.z, W.w));
+                    w_small = w_small && wm < (float)(kRcpTab - kMaxBatch - 1);
+                    w_table = w_table && wm < (float)(kRcpBig - kMaxBatch - 1);
+                } else {
+                    w_small = w_small && small_int(W.x) && small_int(W.y) && small_int(W.z) && small_int(W.w);
+                    w_table = w_table && table_int(W.x) && table_int(W.y) && table_int(W.z) && table_int(W.w);
+                    c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
+                }
+                ts[4 * h + 0] = T.x; ts[4 * h + 1] = T.y; ts[4 * h + 2] = T.z; ts[4 * h + 3] = T.w;
+                cs[4 * h + 0] = C.x; cs[4 * h + 1] = C.y; cs[4 * h + 2] = C.z; cs[4 * h + 3] = C.w;
+            }
+            // Fast paths (wave-uniform; weights grow by one per frame, so the limits leave room
+            // for a whole batch): every lane's weights are small integers -> RN(1/wn) from the LDS
+            // table and Markstein quotients; past the LDS part (a weight of the wave >= 4087) the
+            // same from the HBM table; and, for RGB8 frames, every colour is canonical (an integer
+            // B*65536+G*256+R < 2^24) -> the same for the three colour channels, in f32 with
+            // RN32(1/wn) = f32(RN64(1/wn)) (checked for every table entry by the CPU tests).
+            fast_t = OW1 && s_rcp && __ballot(!w_small) == 0;
+            table_t = OW1 && s_rcp && !fast_t && __ballot(!w_table) == 0;
+            fast_c = CK == 0 && (fast_t || table_t) && __ballot(!c_canon) == 0;
+        }
+#pragma unroll
+        for (int h = 0; h < kH; ++h) loaded[h] |= need[h];
+        if (HASH) {
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) touched |= okv[k] ? 1u << k : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < NZ; ++k) nupd += (unsigned)__popcll(__ballot(okv[k]));  // (wave total, scalar)
         // phase 5: update in registers, straight-line; invalid steps keep their old values.
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
-        // Fast paths (wave-uniform): every lane's weights are small integers -> RN(1/wn) from the
-        // LDS table and Markstein quotients; and, for RGB8 frames, every colour is canonical
-        // (an integer B*65536+G*256+R < 2^24) -> the same for the three colour channels, in f32
-        // with RN32(1/wn) = f32(RN64(1/wn)) (checked for every table entry by the CPU tests).
-        // Past the LDS part (a weight of the wave >= 4087) the same from the HBM table, in code of
-        // its own so the common path keeps its straight-line shape.
-        const bool fast_t = OW1 && s_rcp && __ballot(!w_small) == 0;
-        const bool table_t = OW1 && s_rcp && !fast_t && __ballot(!w_table) == 0;
-        const bool fast_c = CK == 0 && (fast_t || table_t) && __ballot(!c_canon) == 0;
-        float tq[NZ], rws[NZ];  // rws: RN32(1/wn) for the colour quotients
-        if (fast_t) {
+        float wnv[NZ], tqv[NZ], cnv[NZ];  // the step's new weight, tsdf and colour (if it updates)
+        if (fast_c) {
+            // Steps in pairs (k, k+1) on the packed f32 ALU (v_pk_*: two lanes' worth per
+            // instruction): w + 1, w * t, the table offset 8 * (w + 1), and the colour channels'
+            // numerators and Markstein quotients.  Every value is an integer < 2^24 or the exact
+            // f32 expression of the scalar form, so the results are bit-identical to it.
+            // RN(1/wn) from the LDS table, or from the HBM table past its limit through a buffer
+            // load (a different instruction, so the two are never merged into a flat load)
+            const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)v.rcp, 0, kRcpBig * 8, kBufDword3);
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) {
-                const float wn = ws[k] + 1.0f;
-                const double y = s_rcp[(int)wn];
-                const double num = (double)(ws[k] * ts[k]) + dist[k];
-                tq[k] = (float)div_rn(num, (double)wn, y);
-                rws[k] = (float)y;
-            }
-        } else if (table_t) {
+            for (int k = 0; k < NZ; k += 2) {
+                const f2 w2 = {ws[k], ws[k + 1]};
+                const f2 a8 = pk_fma(w2, f2{8.0f, 8.0f}, f2{8.0f, 8.0f});  // byte offsets 8 * (w + 1)
+                const unsigned o0 = (unsigned)a8.x, o1 = (unsigned)a8.y;
+                double y[2];
+                if (fast_t) {
+                    y[0] = *(const double*)((const char*)s_rcp + o0);
+                    y[1] = *(const double*)((const char*)s_rcp + o1);
+                } else {
+                    y[0] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o0, 0, 0));
+                    y[1] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o1, 0, 0));
+                }
+                const f2 wn2 = w2 + 1.0f;
+                const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
+                f2 r2;
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) {
-                const float wn = ws[k] + 1.0f;
-                const double y = v.rcp[(int)wn];
-                const double num = (double)(ws[k] * ts[k]) + dist[k];
-                tq[k] = (float)div_rn(num, (double)wn, y);
-                rws[k] = (float)y;
+                for (int j = 0; j < 2; ++j) {
+                    const double num = (double)wt2[j] + dist[k + j];
+                    tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
+                    r2[j] = (float)y[j];
+                }
+                // colour (grid_fusion.py:302-314): float32, round half to even; decoded by bytes
+                // (v_cvt_f32_ubyte{0,1,2}), exact integer numerators by FMA, Markstein quotients;
+                // the average is <= 255, so min(255, .) is a no-op
+                const unsigned c0 = (unsigned)cs[k], c1 = (unsigned)cs[k + 1];
+                const f2 ob = {(float)((c0 >> 16) & 0xFFu), (float)((c1 >> 16) & 0xFFu)};
+                const f2 nb = {(float)((cpx[k] >> 16) & 0xFFu), (float)((cpx[k + 1] >> 16) & 0xFFu)};
+                const f2 rb = rint2(div_rn32x2(pk_fma(w2, ob, nb), wn2, r2));
+                const f2 og = {(float)((c0 >> 8) & 0xFFu), (float)((c1 >> 8) & 0xFFu)};
+                const f2 ng = {(float)((cpx[k] >> 8) & 0xFFu), (float)((cpx[k + 1] >> 8) & 0xFFu)};
+                const f2 rg = rint2(div_rn32x2(pk_fma(w2, og, ng), wn2, r2));
+                const f2 orr = {(float)(c0 & 0xFFu), (float)(c1 & 0xFFu)};
+                const f2 nr = {(float)(cpx[k] & 0xFFu), (float)(cpx[k + 1] & 0xFFu)};
+                const f2 rr = rint2(div_rn32x2(pk_fma(w2, orr, nr), wn2, r2));
+                const f2 cn2 = pk_fma(rb, f2{65536.0f, 65536.0f}, pk_fma(rg, f2{256.0f, 256.0f}, rr));
+                wnv[k] = wn2.x;
+                wnv[k + 1] = wn2.y;
+                cnv[k] = cn2.x;
+                cnv[k + 1] = cn2.y;
             }
         } else {
+            // the exact paths: non-canonical colours or weights (table quotients where the weights
+            // allow them, else IEEE divisions)
 #pragma unroll
             for (int k = 0; k < NZ; ++k) {
-                const float wn = OW1 ? ws[k] + 1.0f : (float)((double)ws[k] + fr.ow);
-                const double num = (double)(ws[k] * ts[k]) + (OW1 ? dist[k] : fr.ow * dist[k]);
-                tq[k] = (float)(num / (double)wn);
-                rws[k] = 0.0f;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) {
-            const bool ok = (vmask >> k) & 1u;
-            const float w_old = ws[k];
-            const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
-            const float tn = tq[k];
-            // colour (grid_fusion.py:302-314): float32 throughout, round half to even
-            float nb, ng, nr;
-            if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
-                nr = (float)(cpx[k] & 0xFFu);
-                ng = (float)((cpx[k] >> 8) & 0xFFu);
-                nb = (float)((cpx[k] >> 16) & 0xFFu);
-            } else {
-                const float nc = __uint_as_float(cpx[k]);
-                nb = floorf(nc / 65536.0f);
-                ng = floorf((nc - nb * 65536.0f) / 256.0f);
-                nr = nc - nb * 65536.0f - ng * 256.0f;
-            }
-            float cn;
-            if (fast_c) {
-                // canonical colours and integer weights < 65528: decode by bytes, exact integer
-                // numerators by FMA, Markstein quotients (b, g packed); every value is an integer
-                // < 2^24, so each step equals the reference's f32 expression, and the average is
-                // <= 255, so min(255, .) is a no-op
-                const unsigned cu = (unsigned)cs[k];
-                const float rw = rws[k];
-                const float2 o_bg = make_float2((float)((cu >> 16) & 0xFFu), (float)((cu >> 8) & 0xFFu));
-                const float o_r = (float)(cu & 0xFFu);  // v_cvt_f32_ubyte{0,1,2}
-                const float2 n_bg = make_float2(nb, ng);
-                const float2 w2 = make_float2(w_old, w_old), wn2 = make_float2(wn, wn), r2 = make_float2(rw, rw);
-                const float2 num_bg = fma2(w2, o_bg, n_bg);
-                const float2 q0 = num_bg * r2;
-                const float2 q = fma2(fma2(-q0, wn2, num_bg), r2, q0);
-                const float cr = rintf(div_rn32(fmaf(w_old, o_r, nr), wn, rw));
-                cn = fmaf(rintf(q.x), 65536.0f, fmaf(rintf(q.y), 256.0f, cr));
-            } else {
+                const float w_old = ws[k];
+                const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
+                const double num = (double)(w_old * ts[k]) + (OW1 ? dist[k] : fr.ow * dist[k]);
+                if (fast_t) tqv[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
+                else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, v.rcp[(int)wn]);
+                else tqv[k] = (float)(num / (double)wn);
+                wnv[k] = wn;
+                // colour (grid_fusion.py:302-314): float32 throughout, round half to even
+                float nb, ng, nr;
+                if (CK == 0) {  // packed uint8 RGB: the fold/decode round trip is exact
+                    nr = (float)(cpx[k] & 0xFFu);
+                    ng = (float)((cpx[k] >> 8) & 0xFFu);
+                    nb = (float)((cpx[k] >> 16) & 0xFFu);
+                } else {
+                    const float nc = __uint_as_float(cpx[k]);
+                    nb = floorf(nc / 65536.0f);
+                    ng = floorf((nc - nb * 65536.0f) / 256.0f);
+                    nr = nc - nb * 65536.0f - ng * 256.0f;
+                }
                 const float co = cs[k];
                 const float ob = floorf(co / 65536.0f);
                 const float og = floorf((co - ob * 65536.0f) / 256.0f);
@@ -899,11 +980,14 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const float cb = fminf(255.0f, rintf((w_old * ob + (OW1 ? nb : fr.ow32 * nb)) / wn));
                 const float cg = fminf(255.0f, rintf((w_old * og + (OW1 ? ng : fr.ow32 * ng)) / wn));
                 const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
-                cn = cb * 65536.0f + cg * 256.0f + cr;
+                cnv[k] = cb * 65536.0f + cg * 256.0f + cr;
             }
-            ws[k] = ok ? wn : ws[k];
-            ts[k] = ok ? tn : ts[k];
-            cs[k] = ok ? cn : cs[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NZ; ++k) {
+            ws[k] = okv[k] ? wnv[k] : ws[k];
+            ts[k] = okv[k] ? tqv[k] : ts[k];
+            cs[k] = okv[k] ? cnv[k] : cs[k];
         }
     }
 #ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
@@ -916,11 +1000,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     if (kHalfHash && __ballot(touched != 0) == 0) return;  // (its block was looked up in advance)
 
     // phase 6: store the changed halves once (a new hash block is written whole: its init)
-    const unsigned st = dirty | ((HASH && is_new) ? kHalves : 0u);
     const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
 #pragma unroll
-    for (int h = 0; h < NZ / 4; ++h) {
-        if (!((st >> h) & 1u)) continue;
+    for (int h = 0; h < kH; ++h) {
+        if (!loaded[h]) continue;
         *(float4*)(pool.weight + base + 4 * h) = make_float4(ws[4 * h], ws[4 * h + 1], ws[4 * h + 2], ws[4 * h + 3]);
         *(float4*)(pool.tsdf + base + 4 * h) = make_float4(ts[4 * h], ts[4 * h + 1], ts[4 * h + 2], ts[4 * h + 3]);
         *(float4*)(pool.color + base + 4 * h) = make_float4(cs[4 * h], cs[4 * h + 1], cs[4 * h + 2], cs[4 * h + 3]);
@@ -938,12 +1021,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             else if (mine) atomicOr(o, mine);
         }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) nupd += __shfl_xor(nupd, off);
-    if (lane == 0) {
-        atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
-        atomicAdd(&s_stat[ST_TOUCHED], 1ull);
-    }
+    if (lane == 0) atomicAdd(&s_stat[ST_TOUCHED], 1ull);
 }
 
 __device__ inline void flush_stats(unsigned long long* s_stat, unsigned long long* stats) {
@@ -1033,16 +1111,32 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, Li
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
+__device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
+                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
+                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
+                                       unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd);
+template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                       unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
-    constexpr int parts = 8 / NZ;  // waves per listed brick
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
+    unsigned nupd = 0;  // the wave's voxel updates over all its items (ST_VOXELS; wave-uniform)
+    integrate_items<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
+                                           s_next, wg, n_wg, res, nupd);
+    if (lane_id() == 0 && nupd) atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
+}
+
+template <bool HASH, int DK, int CK, bool OW1, int NZ>
+__device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
+                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
+                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
+                                       unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd) {
+    constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
             integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
-                                                   s_stat, s_rcp);
+                                                   s_stat, s_rcp, nupd);
         return;
     }
     // k_cull's list: one sub-list per cost class (frames kept, 1..kMaxBatch), taken most frames
@@ -1075,7 +1169,7 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
             while (c > 0 && (unsigned)k - k0 >= ncls[c]) k0 += ncls[c--];
             // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
             integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
-                                                   (int)(j % parts) * NZ, s_stat, s_rcp, res);
+                                                   (int)(j % parts) * NZ, s_stat, s_rcp, nupd, res);
         }
         return;
     }
@@ -1083,7 +1177,7 @@ __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool&
         const unsigned k = (unsigned)(e / parts);
         while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
         integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
-                                               (e % parts) * NZ, s_stat, s_rcp, res);
+                                               (e % parts) * NZ, s_stat, s_rcp, nupd, res);
     }
 }
 

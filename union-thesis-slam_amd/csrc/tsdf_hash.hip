@@ -98,6 +98,12 @@ struct VArray {
 struct tsdf_hash {
     Base b;
     Table t{};          // device view (pointers + capacity)
+    // The table size the API speaks of (map_size, hash_fusion.py:34-36): hash_function()'s modulus,
+    // doubled by double_table_size and by the 0.75 load-factor policy.  The device table has
+    // t.capacity = the next power of two >= map_size slots, so the home slot and the shard owner are
+    // a mask and a shift in every kernel, whatever size the caller asked for (the reference's
+    // default 10^6 and the demo's 2*10^6 included).
+    long long map_size = 0;
     PoolState host_st{};
     ListEntry* d_list = nullptr;  // re-run list
     int list_cap = 0;
@@ -118,8 +124,16 @@ struct tsdf_hash {
     // exactly later (its batch's frames are gone), so it is reported as TSDF_E_CAPACITY.
     PoolReport* h_rb = nullptr;   // host view of the report slots (hipHostMalloc, mapped)
     long long seq = 0;            // allocating launches issued so far
-    long long rb_used = -1;       // live blocks in the last report read
-    long long max_delta = 0;      // largest growth of live blocks between two reports
+    long long rb_used = -1;       // live blocks in the last report read (or at the last sync check)
+    long long deltas[4] = {};     // growth of live blocks over the last four reports / checks
+    int n_delta = 0;
+    void note_live(long long used) {  // a new live-block count: remember its growth
+        if (rb_used >= 0 && used > rb_used) deltas[n_delta++ & 3] = used - rb_used;
+        rb_used = used;
+    }
+    long long recent_growth() const {  // the largest of the recent growths (at least 256 blocks)
+        return std::max<long long>({deltas[0], deltas[1], deltas[2], deltas[3], 256});
+    }
     long long tomb_est = 0;       // PoolState::tombs at the last read (only remove() adds tombstones)
     bool async_pending = false;   // asynchronous launches since the last overflow check
     // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
@@ -137,6 +151,15 @@ struct tsdf_hash {
 };
 
 namespace {
+
+// Vol::canon over the allocated blocks after a set or an import (blocks past pool_top are
+// initialised when they are handed out)
+int recheck_canon(tsdf_hash* h) {
+    PoolState st{};
+    TSDF_HIP(hipMemcpyAsync(&st, h->t.st, sizeof(st), hipMemcpyDeviceToHost, h->b.stream));
+    TSDF_HIP(hipStreamSynchronize(h->b.stream));
+    return h->b.check_canon(st.pool_top * kBrickVox);
+}
 
 struct InfoDev {
     unsigned long long used, tomb, displaced, max_probe, entries;
@@ -453,6 +476,15 @@ int read_state(tsdf_hash* h) {
     return TSDF_OK;
 }
 
+// The size the pool grows to when it needs room for `need` blocks.  Mapped chunks (VMM) cost no
+// copy and no drain, so the pool follows the live blocks closely: 1/16 over the need, which the
+// callers size as the live blocks plus the growth of the batches in flight; the copy path
+// doubles (each growth copies the whole pool).
+long long pool_target(const tsdf_hash* h, long long need) {
+    if (!h->vmm) return std::max(h->t.max_blocks * 2, need);
+    return std::max(h->t.max_blocks, need + need / 16);
+}
+
 int grow_pool(tsdf_hash* h, long long new_max) {
     Base& B = h->b;
     Table& t = h->t;
@@ -526,6 +558,19 @@ int resize_table(tsdf_hash* h, long long new_cap) {
     return TSDF_OK;
 }
 
+long long next_pow2(long long n) {
+    long long p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// The load-factor policy's doubling: the API size and the device slots together.
+int grow_table(tsdf_hash* h) {
+    TSDF_TRY(resize_table(h, next_pow2(2 * h->map_size)));
+    h->map_size *= 2;
+    return TSDF_OK;
+}
+
 int info_raw(tsdf_hash* h, InfoDev* out) {
     Base& B = h->b;
     InfoDev* d = nullptr;
@@ -540,17 +585,21 @@ int info_raw(tsdf_hash* h, InfoDev* out) {
     return TSDF_OK;
 }
 
-// Grow whatever ran out (reference policy: keep slots used below 0.75 of capacity, like
+// Grow whatever ran out (reference policy: keep the keys below 0.75 of the table size, like
 // needs_resize, hash_fusion.py:156-161), then re-run the bricks that were skipped.
 // Live keys = blocks handed out and not freed; tombstones are bounded by PoolState::tombs -- no
 // table scan per batch (k_info over 2^22 slots cost 1.5 ms).
 int ensure_room(tsdf_hash* h, bool fresh = false) {
     if (!fresh) TSDF_TRY(read_state(h));  // fresh: host_st was read after the stream's last launch
     const long long live = h->host_st.pool_top - h->host_st.free_count;
-    // the block pool keeps the same headroom as the table: live blocks below 0.75 of it
-    if ((double)(live + 64) >= 0.75 * (double)h->t.max_blocks) TSDF_TRY(grow_pool(h, h->t.max_blocks * 2));
-    if ((double)(live + h->host_st.tombs) >= h->max_load * (double)h->t.capacity)
-        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+    h->note_live(live);
+    // the block pool keeps room for the next batches' growth: with mapped chunks about two
+    // batches' worth over the live blocks (a batch that still runs out is re-run exactly after
+    // growing, hash_after_batch); the copy path keeps the live blocks below 0.75 of the pool
+    const long long step = h->recent_growth();
+    if (h->vmm ? live + 2 * step > h->t.max_blocks : (double)(live + 64) >= 0.75 * (double)h->t.max_blocks)
+        TSDF_TRY(grow_pool(h, pool_target(h, live + 3 * step)));
+    while ((double)(live + h->host_st.tombs) >= h->max_load * (double)h->map_size) TSDF_TRY(grow_table(h));
     return TSDF_OK;
 }
 
@@ -602,14 +651,14 @@ int async_room(tsdf_hash* h, long long s) {
     TSDF_TRY(wait_report(h, s - 2, &r));
     if (r.n_overflow > 0) return take_overflow(h);
     const long long used = r.pool_top - r.free_count;
-    if (h->rb_used >= 0 && used > h->rb_used) h->max_delta = std::max(h->max_delta, used - h->rb_used);
-    h->rb_used = used;
-    // (a growth estimate of at least 1/12 of the pool keeps the reference's 0.75 load factor)
-    const long long step = std::max<long long>({h->max_delta, h->t.max_blocks / 12, 64});
+    h->note_live(used);
+    // launches s-1 and s may allocate before the next check: room for three recent growths (the
+    // copy path keeps the pool's 1/12 as a floor of the estimate and doubles)
+    const long long step = h->vmm ? h->recent_growth() : std::max<long long>(h->recent_growth(), h->t.max_blocks / 12);
     const long long need = used + 3 * step;
-    if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, 2 * need)));
-    while ((double)(used + 3 * std::max<long long>(h->max_delta, 64) + h->tomb_est) >= h->max_load * (double)h->t.capacity)
-        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+    if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, pool_target(h, need + step)));
+    while ((double)(used + 3 * h->recent_growth() + h->tomb_est) >= h->max_load * (double)h->map_size)
+        TSDF_TRY(grow_table(h));
     return TSDF_OK;
 }
 
@@ -651,9 +700,9 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
         TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(ListEntry) * n_ov, hipMemcpyDeviceToDevice, B.stream));
         TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
         if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
-            TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * n_ov)));
+            TSDF_TRY(grow_pool(h, pool_target(h, h->host_st.pool_top + 2 * n_ov)));
         else
-            TSDF_TRY(resize_table(h, h->t.capacity * 2));
+            TSDF_TRY(grow_table(h));
         launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
         TSDF_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
@@ -768,8 +817,8 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
                           frame_bytes_color(ck, H, W) * n_frames, flags));
     CallGuard guard(B, flags);
-    // (the fused launch is built for power-of-two table sizes, the library's own; a table resized
-    // to another size runs the in-line kernels)
+    B.note_frames(ck, nullptr, n_frames, 1.0);
+    // (the fused launch is built for power-of-two table sizes: every device table is one)
     const auto p2 = [](long long n) { return n > 0 && (n & (n - 1)) == 0; };
     bool fused = h->fused && ck == TSDF_COLOR_RGB8 && W % 4 == 0 && n_frames > 0 && p2(h->t.capacity) &&
                  p2(h->t.shard_cap);
@@ -865,12 +914,12 @@ int insert_block_keys(tsdf_hash* h, const std::vector<unsigned long long>& keys,
     TSDF_TRY(read_state(h));
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
-    while ((double)(inf.used + inf.tomb + nk) >= h->max_load * (double)h->t.capacity) {
-        TSDF_TRY(resize_table(h, h->t.capacity * 2));
+    while ((double)(inf.used + inf.tomb + nk) >= h->max_load * (double)h->map_size) {
+        TSDF_TRY(grow_table(h));
         TSDF_TRY(info_raw(h, &inf));
     }
     if (h->host_st.pool_top + nk > h->t.max_blocks - h->host_st.free_count)
-        TSDF_TRY(grow_pool(h, std::max(h->t.max_blocks * 2, h->host_st.pool_top + 2 * nk)));
+        TSDF_TRY(grow_pool(h, pool_target(h, h->host_st.pool_top + 2 * nk)));
     void* dkeys;
     TSDF_TRY(upload(h, keys.data(), sizeof(unsigned long long) * nk, &dkeys));
     bufs.add(dkeys);
@@ -922,13 +971,14 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         h->b.vol.n_shards = n_shards;
         if (max_blocks <= 0) max_blocks = std::min<long long>(h->b.n_bricks, 1 << 16);
         max_blocks = std::max<long long>(std::min<long long>(max_blocks, h->b.n_bricks), 64);
-        t.capacity = capacity;
-        t.shard_cap = capacity;
+        h->map_size = capacity;
+        t.capacity = next_pow2(capacity);
+        t.shard_cap = t.capacity;
         t.max_blocks = max_blocks;
         t.int_bits = int_bits;
         t.overflow_cap = (int)std::min<long long>(h->b.n_bricks, 1ll << 30);
-        hipError_t e = hipMalloc(&t.keys, sizeof(unsigned long long) * capacity);
-        if (e == hipSuccess) e = hipMalloc(&t.vals, sizeof(int) * capacity);
+        hipError_t e = hipMalloc(&t.keys, sizeof(unsigned long long) * t.capacity);
+        if (e == hipSuccess) e = hipMalloc(&t.vals, sizeof(int) * t.capacity);
         if (e == hipSuccess) e = hipMalloc(&t.overflow, sizeof(ListEntry) * (size_t)t.overflow_cap);
         if (e == hipSuccess) e = hipMalloc(&t.st, sizeof(PoolState));
         // the pool: address ranges for every brick of the volume, backed as it grows
@@ -1018,9 +1068,11 @@ int tsdf_hash_reset(tsdf_hash_t* h) {
     B.frames = 0;
     std::memset(&h->host_st, 0, sizeof(h->host_st));
     h->rb_used = -1;
-    h->max_delta = 0;
+    std::fill(std::begin(h->deltas), std::end(h->deltas), 0ll);
+    h->n_delta = 0;
     h->tomb_est = 0;
     h->async_pending = false;
+    B.vol.canon = 1;
     return TSDF_OK;
 }
 
@@ -1034,6 +1086,8 @@ int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const
     if (flags & TSDF_DEFER) {
         if (flags & TSDF_DEVICE_PTRS) return set_error(TSDF_E_ARG, "TSDF_DEFER takes host frames only");
         if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(hash_flush(h));
+        // a pending batch's re-run reads its staging slots: settle it before they are reallocated
+        if (h->pend.on && !B.stage_fits(depth_kind, color_kind, height, width)) TSDF_TRY(hash_settle(h));
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1
         TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0));
         if (B.dfr.n == kMaxBatch) TSDF_TRY(hash_flush(h, false));
@@ -1122,6 +1176,7 @@ int tsdf_hash_insert(tsdf_hash_t* h, const int64_t* ijk, int64_t n, const float*
     TSDF_HIP(hipStreamSynchronize(B.stream));
     for (long long i = 0; i < nk; ++i)
         if (blk[i] < 0) return set_error(TSDF_E_CAPACITY, "hash insert failed (table or pool full)");
+    if (weight_ || color_) TSDF_TRY(recheck_canon(h));
     if (slot || local) {
         for (int64_t i = 0; i < n; ++i) {
             const int64_t x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
@@ -1171,7 +1226,11 @@ int tsdf_hash_resize(tsdf_hash_t* h, int64_t new_capacity) {
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
     if (new_capacity <= (int64_t)inf.used) return set_error(TSDF_E_ARG, "new capacity too small");
-    return resize_table(h, new_capacity);
+    if (new_capacity > (1ll << 40)) return set_error(TSDF_E_ARG, "capacity out of range");
+    const long long slots = next_pow2(new_capacity);
+    if (slots != h->t.capacity) TSDF_TRY(resize_table(h, slots));
+    h->map_size = new_capacity;
+    return TSDF_OK;
 }
 
 int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out) {
@@ -1181,7 +1240,8 @@ int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out) {
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
     TSDF_TRY(read_state(h));
-    out->capacity = h->t.capacity;
+    out->capacity = h->map_size;
+    out->slots = h->t.capacity;
     out->used = (int64_t)inf.used;
     out->tombstones = (int64_t)inf.tomb;
     out->displaced = (int64_t)inf.displaced;
@@ -1337,6 +1397,7 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
     TSDF_HIP(hipStreamSynchronize(B.stream));
     for (int64_t i = 0; i < n_blocks; ++i)
         if (blk[i] < 0) return set_error(TSDF_E_CAPACITY, "hash import failed (table or pool full)");
+    if (weight_ || color_) TSDF_TRY(recheck_canon(h));
     return TSDF_OK;
 }
 

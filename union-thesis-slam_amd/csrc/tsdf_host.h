@@ -30,6 +30,9 @@ int set_error(int code, const char* fmt, ...);
         if (r_ != TSDF_OK) return r_; \
     } while (0)
 
+inline size_t frame_bytes_depth(int dk, int H, int W) { return (size_t)H * W * (dk == TSDF_DEPTH_U16_MM ? 2 : 8); }
+inline size_t frame_bytes_color(int ck, int H, int W) { return (size_t)H * W * (ck == TSDF_COLOR_RGB8 ? 3 : 4); }
+
 struct PyrLayout {
     int off[kPyrLevels + 1];
     int w[kPyrLevels + 1];
@@ -116,6 +119,10 @@ struct Base {
     int defer_push(const void* depth, int dk, const void* color, int ck, int H, int W,
                    const double* K, const double* T, double ow);
     int stage_alloc(size_t dbytes, size_t cbytes);  // bounce + device staging slots (per frame)
+    bool stage_fits(int dk, int ck, int H, int W) const {  // frames of this size need no reallocation
+        return st_depth_bytes >= frame_bytes_depth(dk, H, W) * kMaxBatch &&
+               st_color_bytes >= frame_bytes_color(ck, H, W) * kMaxBatch;
+    }
 
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
              double vs, double trunc);
@@ -155,6 +162,14 @@ struct Base {
         return (unsigned)n;
     }
     int read_stats(tsdf_stats_t* out, int reset);
+    // Vol::canon from the first n_vox voxels of the pool (after a set or an import; synchronous)
+    int check_canon(long long n_vox);
+    // a call whose frames may write non-canonical state (obs_weight != 1, folded f32 colour)
+    void note_frames(int ck, const double* ow, int n, double ow_default) {
+        if (ck != TSDF_COLOR_RGB8) vol.canon = 0;
+        for (int i = 0; i < n; ++i)
+            if ((ow ? ow[i] : ow_default) != 1.0) vol.canon = 0;
+    }
     int set_profiling(int on);
     void release();
 };
@@ -198,8 +213,6 @@ struct CallGuard {
     }
 };
 
-inline size_t frame_bytes_depth(int dk, int H, int W) { return (size_t)H * W * (dk == TSDF_DEPTH_U16_MM ? 2 : 8); }
-inline size_t frame_bytes_color(int ck, int H, int W) { return (size_t)H * W * (ck == TSDF_COLOR_RGB8 ? 3 : 4); }
 
 int check_frame_args(const void* depth, int dk, const void* color, int ck, int H, int W,
                      const double* K, const double* Tinv);

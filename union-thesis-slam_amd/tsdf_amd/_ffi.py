@@ -52,7 +52,7 @@ class HashInfo(ctypes.Structure):
     _fields_ = [("capacity", ctypes.c_int64), ("used", ctypes.c_int64),
                 ("tombstones", ctypes.c_int64), ("displaced", ctypes.c_int64),
                 ("max_probe", ctypes.c_int64), ("blocks_in_pool", ctypes.c_int64),
-                ("pool_capacity", ctypes.c_int64), ("entries", ctypes.c_int64)]
+                ("pool_capacity", ctypes.c_int64), ("entries", ctypes.c_int64), ("slots", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -246,7 +246,10 @@ class HashTable:
         if n == 0:
             return
         if dev:
-            ptrs = [None if a is None else a.contiguous().data_ptr() for a in (bxyz, tsdf, weight, color, occ)]
+            # the contiguous copies must outlive the call (a temporary's memory could be reused
+            # before the library reads it)
+            keep = [None if a is None else a.contiguous() for a in (bxyz, tsdf, weight, color, occ)]
+            ptrs = [None if a is None else a.data_ptr() for a in keep]
         else:
             arrs = [np.ascontiguousarray(bxyz, np.int32)] + [
                 None if a is None else np.ascontiguousarray(a, np.float32) for a in (tsdf, weight, color)] + [
@@ -254,6 +257,8 @@ class HashTable:
             ptrs = [_ffi.ptr(a) for a in arrs]
         _ffi.call("tsdf_hash_import_blocks", self._h, ptrs[0], n, ptrs[1], ptrs[2], ptrs[3], ptrs[4],
                   _ffi.DEVICE_PTRS if dev else 0)
+        if dev:
+            del keep
 
     # ------------------------------------------------------------------ export
     def get_volume(self):

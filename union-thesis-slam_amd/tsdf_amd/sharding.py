@@ -66,21 +66,46 @@ def ref_hash(x, y, z, n: int, int_bits: int = 64):
 
 def hash_owner(bx, by, bz, capacity: int, n_shards: int, int_bits: int = 64):
     """Shard owning block (bx,by,bz): the bucket range its home slot falls in (the same
-    arithmetic as k_cull<true>).  `capacity` is the table's capacity at create: ownership is
-    fixed then (Table::shard_cap) and does not follow later resizes, so no block ever moves
-    between shards."""
-    home = ref_hash(bx, by, bz, capacity, int_bits)
-    return (home * n_shards) // capacity
+    arithmetic as k_cull<true>).  `capacity` is the table size at create (map_size); the device
+    table has S = the power of two >= it slots and the home slot is the hash floor-mod S.
+    Ownership is fixed at create (Table::shard_cap) and does not follow later resizes, so no
+    block ever moves between shards."""
+    slots = 1 << (int(capacity) - 1).bit_length()
+    home = ref_hash(bx, by, bz, slots, int_bits)
+    return (home * n_shards) // slots
+
+
+_BUFFER_DEVICE = None
+
+
+def set_buffer_device(device):
+    """Override where collective buffers live (None: by backend, _device).  The GPU tests' 2-rank
+    job runs gloo with device buffers ("cuda"), so the branches the RCCL run takes -- rows read
+    into device tensors, halos and blocks handed to the library as device pointers -- execute on
+    the one-GPU box too; gloo moves device tensors itself for broadcast, all_reduce and
+    all_gather, and through host copies for gather and point-to-point (_gloo_staged)."""
+    global _BUFFER_DEVICE
+    _BUFFER_DEVICE = device
 
 
 def _device(group=None):
     """Where collective buffers live: the rank's GPU under RCCL ("nccl"), host memory under gloo
-    (the CPU tests)."""
+    (the CPU tests), or the set_buffer_device override."""
     import torch
     import torch.distributed as dist
+    if _BUFFER_DEVICE is not None:
+        d = torch.device(_BUFFER_DEVICE)
+        return torch.device("cuda", torch.cuda.current_device()) if d.type == "cuda" and d.index is None else d
     if dist.get_backend(group) == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
+
+
+def _gloo_staged(group=None):
+    """Device buffers on gloo: gather and point-to-point go through host copies (gloo has no
+    device-tensor path for them); RCCL takes the device tensors directly."""
+    import torch.distributed as dist
+    return _device(group).type == "cuda" and dist.get_backend(group) == "gloo"
 
 
 def _all_x_index(x_index, group=None):
@@ -162,6 +187,7 @@ def exchange_halo(vol, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = _device(group)
+    staged = _gloo_staged(group)
     X = int(vol._vol_dim[0])
     Y, Z = int(vol._local_dim[1]), int(vol._local_dim[2])
     need = vol.mesh_halo_rows(X)
@@ -185,17 +211,22 @@ def exchange_halo(vol, group=None):
             if dev.type == "cuda":
                 sb = torch.empty((2, len(lr), Y, Z), dtype=torch.float32, device=dev)
                 vol.get_rows(lr, out=[sb[0], None, sb[1]])
+                torch.cuda.synchronize()
+                if staged:
+                    sb = sb.cpu()
             else:
                 t, _, c = vol.get_rows(lr, weight=False)
                 sb = torch.from_numpy(np.stack([t, c]))
             ops.append(dist.P2POp(dist.isend, sb, p, group=group))
         if take:
-            rb = torch.empty((2, len(take), Y, Z), dtype=torch.float32, device=dev)
+            rb = torch.empty((2, len(take), Y, Z), dtype=torch.float32, device="cpu" if staged else dev)
             recv[p] = (take, rb)
             ops.append(dist.P2POp(dist.irecv, rb, p, group=group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    if staged:
+        recv = {p: (tk, rb.to(dev)) for p, (tk, rb) in recv.items()}
     if dev.type == "cuda":
         torch.cuda.synchronize()
     missing = [g for g in need if owner_of[g] < 0]
@@ -271,13 +302,16 @@ def merge_hash_shards(ht, make_table, group=None, dst: int = 0):
     n_max = max(counts)
     merged = make_table() if rank == dst else None
     fields = []
+    staged = _gloo_staged(group)
     for b in blocks:  # one field at a time keeps the padded buffers small
         pad = torch.zeros((n_max,) + tuple(b.shape[1:]), dtype=b.dtype, device=dev)
         pad[: b.shape[0]] = b
+        if staged:
+            pad = pad.cpu()
         got = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
         dist.gather(pad, got, dst=dst, group=group)
         if rank == dst:
-            fields.append(torch.cat([g[:c] for g, c in zip(got, counts)]))
+            fields.append(torch.cat([g[:c] for g, c in zip(got, counts)]).to(dev))
     if rank != dst:
         return None
     if dev.type == "cuda":
