@@ -45,7 +45,10 @@ VOXEL = 0.02
 PIX = 640 * 480
 BATCH = 8  # frames per step (kMaxBatch)
 WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) into 512^3 @ 2 cm dense grid"
-PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r02.json")
+# the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), used when their
+# workload matches: DRAM-side traffic (FETCH_SIZE / WRITE_SIZE) and VALU issue (SQ counters)
+PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r03.json")
+SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r03.json")
 
 
 def log(*a):
@@ -286,6 +289,26 @@ def main():
                 roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
                 roof["traffic_source"] = (os.path.relpath(PMC_PROFILE, REPO) + " (separate rocprofv3 --pmc "
                                           "FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 rule)")
+        if os.path.exists(SQ_PROFILE):
+            with open(SQ_PROFILE) as fh:
+                q = json.load(fh)
+            med = q.get("median_per_launch", {})
+            if q.get("workload") == WORKLOAD and med.get("SQ_INSTS_VALU"):
+                vox_launch = st["voxel_updates"] / st["kernel_launches"]
+                roof["valu"] = {
+                    "valu_busy": q["valu_busy_per_simd"],
+                    "valu_wave_insts_per_launch": round(med["SQ_INSTS_VALU"]),
+                    "valu_lane_insts_per_voxel_update": round(64.0 * med["SQ_INSTS_VALU"] / vox_launch, 1),
+                    "source": os.path.relpath(SQ_PROFILE, REPO) + " (rocprofv3 --pmc SQ pass of the same "
+                              "kernel and workload; busy = SQ_ACTIVE_INST_VALU x 4 / SIMD cycles)"}
+                # the binding resource: the one closer to its peak (VALU issue vs measured DRAM bytes;
+                # the algorithmic bytes above count every update's state traffic, which temporal
+                # batching keeps on chip)
+                if roof.get("traffic_frac") is not None and q["valu_busy_per_simd"] > roof["traffic_frac"]:
+                    roof["bound"] = "valu"
+                    roof["bound_note"] = ("VALU issue-bound: the SIMDs issue VALU in valu_busy of their cycles "
+                                          "while DRAM moves traffic_frac of its peak; achieved/peak/frac are the "
+                                          "algorithmic-bytes HBM roofline of the contract")
     vf_mean = st["voxel_updates"] / Kf
     log(f"[rank {rank}] dense: {Kf} frames in {dt * 1e3:.1f} ms -> {Kf / dt:.0f} frames/s, "
         f"V_f mean {vf_mean:.0f} ({100 * vf_mean / (len(vol.x_index) * X * X):.1f}% of shard), "

@@ -225,6 +225,10 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 /* get_volume (hash_fusion.py:442-463): densify into C-order (X,Y,Z) host arrays; voxels
  * without an entry get tsdf 1, weight 0, colour 0.  Any pointer may be NULL. */
 int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf, float* weight, float* color);
+/* The same densify on the device, into a dense handle of the hash's dims (unsharded; it is reset
+ * first): get_mesh / get_point_cloud of the hash (hash_fusion.py:465-507) then run the dense
+ * handle's marching cubes without a host round trip of the volume. */
+int tsdf_hash_to_dense(tsdf_hash_t* h, tsdf_dense_t* d);
 int tsdf_hash_sync(tsdf_hash_t* h);
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);

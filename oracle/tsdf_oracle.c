@@ -91,10 +91,12 @@ int64_t oracle_dense_integrate_rows(const int64_t* dims, const int64_t* off, con
     p.xmap = xmap;
     const float ow32 = (float)ow; /* NumPy weak-scalar: Python float * f32 array stays f32 */
     int64_t n = 0;
-    int64_t i = 0;
+    /* voxels are independent: (x, y) columns in parallel (OpenMP; the same result on any thread count) */
+#pragma omp parallel for collapse(2) reduction(+ : n) schedule(static)
     for (int64_t ix = 0; ix < dims[0]; ++ix)
         for (int64_t iy = 0; iy < dims[1]; ++iy)
-            for (int64_t iz = 0; iz < dims[2]; ++iz, ++i) {
+            for (int64_t iz = 0; iz < dims[2]; ++iz) {
+                const int64_t i = (ix * dims[1] + iy) * dims[2] + iz;
                 int64_t pix;
                 double z;
                 if (upd) upd[i] = 0;

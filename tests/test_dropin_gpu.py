@@ -208,3 +208,21 @@ def test_f64_device_frames_match_the_u16_encoding():
         assert _same(a, b) and _same(x, b)
     for a, b in zip(h16, g16):
         assert _same(a, b)
+
+
+def test_pool_growth_falls_back_whole_when_one_mapping_fails(monkeypatch):
+    """The pool's five arrays grow together or not at all: a mapping refused for the fourth
+    array (TSDF_HASH_VMM_FAIL=3, a test hook) unmaps the three grown before it, and the pool moves
+    to plain allocations by copy -- the result still equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    monkeypatch.setenv("TSDF_HASH_VMM_FAIL", "3")
+    d, c, poses = _synth(24, start=100)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.04, 1 << 12, max_blocks=256)
+    h.integrate_batch(d, c, K, Tinv)
+    assert h.info()["pool_capacity"] > 256 and h.stats()["bricks_skipped"] > 0
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.04)
+    g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)

@@ -1,12 +1,14 @@
 """Long runs and the per-rank workloads of BASELINE's 8-GPU configs, on one GPU:
 
   * config[3] per rank: cyclic column shard 3 of 8 of the 512^3 @ 2 cm volume over 1000 frames
-    of the bench trajectory, bit-exact against the oracle on rows of the shard;
+    of the bench trajectory, bit-exact against the oracle on rows of the shard; and over 5000
+    frames, where weights cross the LDS reciprocal table's limit by accumulation;
   * the fast-path boundaries: weights around the 4087 limit of the LDS part of the reciprocal
     table and the 65527 limit of the whole table (kRcpTab / kRcpBig, csrc/tsdf_device.h) and
     non-canonical colours, preloaded with set_state;
   * config[4] per rank: bucket-range hash shard 5 of 8 over a 1024^3 @ 1 cm extent with 2^22
-    buckets, against dense slabs (and the oracle) on rows restricted to the shard's blocks;
+    buckets over 500 frames, against dense slabs (and the oracle) on rows restricted to the
+    shard's blocks;
   * the hash's f32 state against the reference's float64 Voxel (voxel.py:19-49) over 500 frames,
     within north_star's 1e-4.
 """
@@ -70,6 +72,38 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
     assert w.max() >= 500 and vol.stats()["list_errors"] == 0
 
 
+def test_config3_rank_shard_5000_frames_crosses_the_table_limit_naturally():
+    """config[3]'s sequence length on one rank: cyclic column shard 3 of 8 of 512^3 @ 2 cm
+    integrates 5000 frames of the bench trajectory (625 batches).  Weights pass the 4087 limit of
+    the LDS part of the reciprocal table by accumulation alone (no preload), so waves move to the
+    HBM table mid-run; the two rows holding the largest weights equal the oracle bit for bit."""
+    from tsdf_amd import grid_fusion, scene, sharding
+    n = 5000
+    depth, rgb, poses = _frames_on_device(n)
+    K = scene.intrinsics()
+    Tinv = np.linalg.inv(poses)
+    bnds = np.array([[0.0, ROOM]] * 3)
+    vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(3, 8))
+    vol.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=False)
+    vol.sync()
+    xi = sharding.columns(3, 8, 512)
+    _, W, _ = vol.get_state()
+    row_max = W.reshape(len(xi), -1).max(1)
+    assert row_max.max() > 4087  # crossed by accumulation
+    pick = np.argsort(row_max)[-2:]  # the two rows with the largest weights
+    rows = xi[np.sort(pick)]
+    del W
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.02, x_index=rows)
+    dh = depth.cpu().numpy().view(np.uint16)
+    ch = rgb.cpu().numpy()
+    del depth, rgb
+    for f in range(n):
+        orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    t, w, c = vol.get_rows(np.searchsorted(xi, rows))
+    assert _same(t, orc._tsdf_vol_cpu) and _same(w, orc._weight_vol_cpu) and _same(c, orc._color_vol_cpu)
+    assert (w > 4087).sum() > 100 and vol.stats()["list_errors"] == 0
+
+
 @pytest.mark.parametrize("batched,w_lo,limit", [(False, 4078, 4087), (True, 4078, 4087),
                                                 (True, 65515, 65527)])
 def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched, w_lo, limit):
@@ -110,11 +144,11 @@ def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched, w_lo
 
 def test_config4_rank_hash_shard_1024_extent():
     """One rank of config[4]: bucket-range shard 5 of 8 over a 1024^3 @ 1 cm extent (2^21 bricks,
-    21-bit key fields up to 127), 2^22 buckets, 40 frames.  On three x rows: a voxel is found iff
+    21-bit key fields up to 127), 2^22 buckets, 500 frames.  On three x rows: a voxel is found iff
     its block's home bucket is in the shard's range and the dense grid updated it, with the dense
     grid's exact values; the dense rows equal the oracle."""
     from tsdf_amd import grid_fusion, hash_fusion, scene, sharding
-    n = 40
+    n = 500
     depth, rgb, poses = _frames_on_device(n, start=300)
     K = scene.intrinsics()
     Tinv = np.linalg.inv(poses)

@@ -75,3 +75,24 @@ def test_hash_mesh_equals_dense_mesh(gf):
             assert np.array_equal(x, y)
     else:  # f32 hash state may differ from the grid's by rounding; meshes agree in topology
         assert abs(len(a[0]) - len(b[0])) <= 0.001 * len(a[0])
+
+
+def test_hash_densifies_on_the_device_like_the_host_export(gf):
+    """tsdf_hash_to_dense (get_mesh / get_point_cloud of the hash without a host round trip)
+    writes exactly get_state()'s volume into a dense handle: integrated blocks, an entry of
+    weight 0 set by add_entries, a removed entry, and a ragged extent (dims not multiples of 8)."""
+    from tsdf_amd import _ffi, hash_fusion
+    bnds = np.array([[-2.56, 1.48], [-2.52, 2.56], [0.0, 5.00]])
+    K = lounge_intrinsics()
+    ht = hash_fusion.HashTable(bnds.copy(), 0.04, 1 << 12)
+    for i in range(2):
+        _, depth, rgb, pose = load_lounge(i)
+        ht.integrate(rgb, depth, K, pose)
+    ht.add_entries([[1, 2, 3], [100, 126, 124]], tsdf=[0.5, -0.25], weight=[0.0, 3.0], color=[7.0, 65793.0])
+    ht.remove_entries([[1, 2, 4]])
+    grid = ht._as_grid()
+    for a, b in zip(grid.get_state(), ht.get_state()):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    other = gf.TSDFVolume(np.array(C1), 0.04)
+    with pytest.raises(_ffi.TSDFError):
+        _ffi.call("tsdf_hash_to_dense", ht._h, other._h)  # dims differ

@@ -264,6 +264,8 @@ struct DevPtrs {
 
 }  // namespace
 
+Base* tsdf::dense_base(tsdf_dense_t* d) { return &d->b; }
+
 extern "C" {
 
 static int dense_create(const int64_t dims[3], const int64_t index_offset[3], int xstride, int xodd,

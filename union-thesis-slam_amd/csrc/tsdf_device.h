@@ -529,12 +529,13 @@ __device__ inline double readlane_f64(double x, int l) {
 
 // Phases 1-3 of one frame for one part (z-steps zoff .. zoff+NZ-1 of a lane's column): project,
 // gather, depth / truncation test.  ok[k]: step k updates its voxel; fills the packed colour
-// texels and the clamped distances of every step.  The per-step conditions stay booleans (lane
+// texels and depth - z of every step (dist_of gives the clamped distance; the integrate computes
+// it only where a voxel needs it).  The per-step conditions stay booleans (lane
 // masks in SGPR pairs): their combinations and wave ballots are scalar instructions, not VALU.
 template <int DK, int CK, int NZ>
 __device__ __forceinline__ void project_part(const Vol& v, const Frame& fr, double px, double py,
                                              const double* pzs, double pz_l, int zoff, bool col_in, int nz,
-                                             unsigned (&cpx)[NZ], double (&dist)[NZ], bool (&ok)[NZ]) {
+                                             unsigned (&cpx)[NZ], double (&diff)[NZ], bool (&ok)[NZ]) {
     constexpr int kPz = NZ < 8 ? NZ : 1;
     // the z term of OpenBLAS's dgemm chain (grid_fusion.py:363-368): exact, it feeds the depth test
     const double a2 = fma(fr.T[9], py, fr.T[8] * px);
@@ -614,13 +615,14 @@ __device__ __forceinline__ void project_part(const Vol& v, const Frame& fr, doub
     // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        const double diff = dep[k] - zc[k];
+        diff[k] = dep[k] - zc[k];
         const bool dpos = DK == 0 ? draw[k] != 0u : dep[k] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
-        ok[k] = cand[k] & dpos & (diff >= -v.trunc);
-        const double dd = div_rn(diff, v.trunc, v.rtrunc);
-        dist[k] = fmin(dd, 1.0);  // np.minimum(1, .) (dd is never NaN)
+        ok[k] = cand[k] & dpos & (diff[k] >= -v.trunc);
     }
 }
+
+// np.minimum(1, (depth - z) / trunc) (grid_fusion.py:284-286; the quotient is never NaN)
+__device__ inline double dist_of(const Vol& v, double diff) { return fmin(div_rn(diff, v.trunc, v.rtrunc), 1.0); }
 
 // Hash z-half waves (NZ = 4, the fused hash launch).  The two halves of a brick are waves 2m and
 // 2m+1 of one workgroup (integrate_list with an even wave count per workgroup) and meet in the
@@ -719,9 +721,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             for (int fi = 0; fi < bt.n && !need; ++fi) {
                 if (!((fmask >> fi) & 1u)) continue;
                 unsigned cpx[NZ];
-                double dist[NZ];
+                double diff[NZ];
                 bool okv[NZ], any = false;
-                project_part<DK, CK, NZ>(v, bt.f[fi], px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist, okv);
+                project_part<DK, CK, NZ>(v, bt.f[fi], px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
 #pragma unroll
                 for (int k = 0; k < NZ; ++k) any |= okv[k];
                 need = __ballot(any) != 0;
@@ -809,9 +811,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         ++d_pairs;
 #endif
         unsigned cpx[NZ];
-        double dist[NZ];
+        double diff[NZ];
         bool okv[NZ];
-        project_part<DK, CK, NZ>(v, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, dist, okv);
+        project_part<DK, CK, NZ>(v, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
         bool need[kH];
 #pragma unroll
         for (int h = 0; h < kH; ++h) need[h] = okv[4 * h] | okv[4 * h + 1] | okv[4 * h + 2] | okv[4 * h + 3];
@@ -908,6 +910,13 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             // RN(1/wn) from the LDS table, or from the HBM table past its limit through a buffer
             // load (a different instruction, so the two are never merged into a flat load)
             const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)v.rcp, 0, kRcpBig * 8, kBufDword3);
+            // Free space (wave-uniform): every updating voxel is at least trunc in front of the
+            // surface (dist = min(1, diff / trunc) = 1 exactly) and still holds tsdf 1, so its new
+            // tsdf is (w * 1 + 1) / (w + 1) = 1 exactly: the distance and tsdf quotients are skipped
+            bool busy = false;
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) busy |= okv[k] & ((diff[k] < v.trunc) | (ts[k] != 1.0f));
+            const bool free_space = __ballot(busy) == 0;
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
                 const f2 w2 = {ws[k], ws[k + 1]};
@@ -922,13 +931,21 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     y[1] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o1, 0, 0));
                 }
                 const f2 wn2 = w2 + 1.0f;
-                const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
                 f2 r2;
+                if (free_space) {
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const double num = (double)wt2[j] + dist[k + j];
-                    tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
-                    r2[j] = (float)y[j];
+                    for (int j = 0; j < 2; ++j) {
+                        tqv[k + j] = ts[k + j];
+                        r2[j] = (float)y[j];
+                    }
+                } else {
+                    const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const double num = (double)wt2[j] + dist_of(v, diff[k + j]);
+                        tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
+                        r2[j] = (float)y[j];
+                    }
                 }
                 // colour (grid_fusion.py:302-314): float32, round half to even; decoded by bytes
                 // (v_cvt_f32_ubyte{0,1,2}), exact integer numerators by FMA, Markstein quotients;
@@ -956,7 +973,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             for (int k = 0; k < NZ; ++k) {
                 const float w_old = ws[k];
                 const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
-                const double num = (double)(w_old * ts[k]) + (OW1 ? dist[k] : fr.ow * dist[k]);
+                const double dist = dist_of(v, diff[k]);
+                const double num = (double)(w_old * ts[k]) + (OW1 ? dist : fr.ow * dist);
                 if (fast_t) tqv[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
                 else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, v.rcp[(int)wn]);
                 else tqv[k] = (float)(num / (double)wn);

@@ -81,6 +81,16 @@ struct VArray {
         mapped = want;
         return TSDF_OK;
     }
+    // undo the mappings made after the array held `n_chunks` chunks (a failed multi-array growth)
+    void unmap_to(size_t n_chunks) {
+        while (chunks.size() > n_chunks) {
+            const auto c = chunks.back();
+            chunks.pop_back();
+            mapped -= c.second;
+            (void)hipMemUnmap(base + mapped, c.second);
+            (void)hipMemRelease(c.first);
+        }
+    }
     void release() {
         size_t off = mapped;
         for (auto it = chunks.rbegin(); it != chunks.rend(); ++it) {
@@ -142,10 +152,28 @@ struct tsdf_hash {
     // block pool on reserved address ranges (tsdf, weight, colour, entry words, free list)
     bool vmm = false;
     VArray va[5];
-    int map_pool(long long n) {  // back blocks [0, n) of every pool array
+    int vmm_fail_at = -1;  // test hook (TSDF_HASH_VMM_FAIL=k): the next growth of array k fails
+    // Back blocks [0, n) of every pool array, all or nothing: if one array cannot grow, the
+    // arrays grown before it are unmapped back to their old size, so the pool stays consistent
+    // for the copy fallback (grow_pool).
+    int map_pool(long long n) {
         const size_t per[5] = {sizeof(float) * kBrickVox, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
                                sizeof(unsigned long long) * 8, sizeof(int)};
-        for (int k = 0; k < 5; ++k) TSDF_TRY(va[k].grow(per[k] * (size_t)n));
+        size_t before[5];
+        for (int k = 0; k < 5; ++k) before[k] = va[k].chunks.size();
+        for (int k = 0; k < 5; ++k) {
+            int r = TSDF_OK;
+            if (k == vmm_fail_at) {
+                vmm_fail_at = -1;
+                r = set_error(TSDF_E_OOM, "pool mapping refused (test hook)");
+            } else {
+                r = va[k].grow(per[k] * (size_t)n);
+            }
+            if (r != TSDF_OK) {
+                for (int j = 0; j < k; ++j) va[j].unmap_to(before[j]);
+                return r;
+            }
+        }
         return TSDF_OK;
     }
 };
@@ -359,6 +387,34 @@ __global__ void k_info(Table t, InfoDev* out) {
         unsigned long long c = 0;
         for (int k = 0; k < 8; ++k) c += __popcll(coh_load(&t.occ[blk * 8 + k]));
         if (c) atomicAdd(&out->entries, c);
+    }
+}
+
+// Densify into a dense handle's brick pool (same dims, so brick b of block (bx,by,bz) is
+// (bx*nb1 + by)*nb2 + bz with the same voxel order inside): one thread per (slot, z-plane of the
+// block); the voxels with an entry are copied, the others keep the dense handle's (1, 0, 0).
+__global__ void k_to_bricks(Vol v, Table t, Pool pool, Pool dst) {
+    const long long total = t.capacity * kBrickEdge;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long s = i >> 3;
+        const int kz = (int)(i & 7);
+        const unsigned long long key = coh_load(&t.keys[s]);
+        if (key == kEmpty || key == kTomb) continue;
+        const long long blk = coh_load(&t.vals[s]);
+        unsigned long long m = coh_load(&t.occ[blk * 8 + kz]);
+        const long long bx = (long long)(key & 0x1FFFFF), by = (long long)((key >> 21) & 0x1FFFFF),
+                        bz = (long long)(key >> 42);
+        const size_t b = (size_t)((bx * v.nb[1] + by) * v.nb[2] + bz);
+        while (m) {
+            const int bit = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const size_t o = b * kBrickVox + bit * 8 + kz;
+            const size_t j = (size_t)blk * kBrickVox + bit * 8 + kz;
+            dst.tsdf[o] = coh_load(&pool.tsdf[j]);
+            dst.weight[o] = coh_load(&pool.weight[j]);
+            dst.color[o] = coh_load(&pool.color[j]);
+        }
     }
 }
 
@@ -1020,6 +1076,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
                           hipGetErrorString(e));
     }
     if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;  // 0: in-line kernels
+    if (const char* e = getenv("TSDF_HASH_VMM_FAIL")) h->vmm_fail_at = atoi(e);  // (after the initial mapping)
     if (const char* e = getenv("TSDF_HASH_MAX_LOAD")) {
         const double ml = atof(e);
         if (ml > 0.0 && ml < 1.0) h->max_load = ml;
@@ -1272,6 +1329,25 @@ int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf_, float* weight_, float* col
     if (weight_) TSDF_HIP(hipMemcpyAsync(weight_, dw, n * sizeof(float), hipMemcpyDeviceToHost, B.stream));
     if (color_) TSDF_HIP(hipMemcpyAsync(color_, dc, n * sizeof(float), hipMemcpyDeviceToHost, B.stream));
     TSDF_HIP(hipStreamSynchronize(B.stream));
+    return TSDF_OK;
+}
+
+int tsdf_hash_to_dense(tsdf_hash_t* h, tsdf_dense_t* d) {
+    if (!h || !d) return set_error(TSDF_E_ARG, "null handle");
+    Base& B = h->b;
+    TSDF_HIP(hipSetDevice(B.device));
+    TSDF_TRY(hash_flush(h));
+    TSDF_TRY(tsdf_dense_sync(d));  // (runs the dense handle's deferred frames first)
+    Base& D = *dense_base(d);
+    for (int a = 0; a < 3; ++a)
+        if (D.vol.dims[a] != B.vol.dims[a] || D.vol.off[a] != 0 || D.vol.xstride != kBrickEdge)
+            return set_error(TSDF_E_ARG, "the dense handle must be an unsharded volume of the hash's dims");
+    if (D.device != B.device) return set_error(TSDF_E_ARG, "the handles live on different devices");
+    TSDF_TRY(tsdf_dense_reset(d));  // (1, 0, 0) everywhere, then the live blocks' entries
+    hipLaunchKernelGGL(k_to_bricks, dim3(4096), dim3(256), 0, B.stream, B.vol, h->t, B.pool, D.pool);
+    TSDF_HIP(hipGetLastError());
+    TSDF_HIP(hipStreamSynchronize(B.stream));
+    D.vol.canon = B.vol.canon;
     return TSDF_OK;
 }
 

@@ -198,6 +198,9 @@ int extract_mesh(Base& B, const Pool& pool, Mesh& m, const MeshDomain& d, const 
 int copy_mesh(Base& B, const Mesh& m, float* verts, float* normals, uint8_t* colors, int32_t* faces,
               int64_t* keys = nullptr);
 
+// The state of a dense handle (tsdf_dense.hip), for the hash's densify into it.
+Base* dense_base(tsdf_dense_t* d);
+
 // end_call on every exit path of an integrate call (error returns included).
 struct CallGuard {
     Base& b;

@@ -96,6 +96,7 @@ SIGNATURES = {
     "tsdf_hash_resize": [_P, _I64],
     "tsdf_hash_info": [_P, _P],
     "tsdf_hash_get_dense": [_P, _P, _P, _P],
+    "tsdf_hash_to_dense": [_P, _P],
     "tsdf_hash_export_blocks": [_P, _P, _P, _P, _P, _P, _P, _I],
     "tsdf_hash_import_blocks": [_P, _P, _I64, _P, _P, _P, _P, _I],
     "tsdf_hash_sync": [_P],

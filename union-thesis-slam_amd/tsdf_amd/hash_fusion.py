@@ -275,13 +275,13 @@ class HashTable:
         return t, w, c
 
     def _as_grid(self):
-        """The densified volume (get_volume, hash_fusion.py:442-463) in a dense device handle."""
-        t, w, c = self.get_state()
+        """The densified volume (get_volume, hash_fusion.py:442-463) in a dense device handle,
+        filled on the device from the live blocks (tsdf_hash_to_dense: no host round trip)."""
         lo = np.asarray(self._vol_bounds, dtype=np.float64)[:, 0]
         bnds = np.stack([lo, lo + (np.asarray(self._vol_dim) - 0.5) * self._voxel_size], axis=1)  # same dims
         with contextlib.redirect_stdout(io.StringIO()):
             vol = grid_fusion.TSDFVolume(bnds, self._voxel_size, device=self.device)
-        vol.set_state(t, w, c)
+        _ffi.call("tsdf_hash_to_dense", self._h, vol._h)
         return vol
 
     def get_mesh(self):
