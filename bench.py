@@ -408,6 +408,8 @@ def main():
         run_timed(ht, depth, rgb, K, Tinv, 0, Wf, F, sync, barrier, False, async_=False)
         hdt = run_timed(ht, depth, rgb, K, Tinv, Wf, Kf, F, sync, barrier, not args.no_profile)
         hs = ht.stats()
+        peak_pool = ht.info()["pool_capacity"]
+        ht.trim()  # the run's end: the pool hands the memory above its live blocks back
         info = ht.info()
         if hs["bricks_skipped"]:
             raise RuntimeError(f"hash table/pool overflowed ({hs['bricks_skipped']} bricks skipped)")
@@ -422,14 +424,16 @@ def main():
                     "load_factor": round(used / (1 << 22), 4),
                     "blocks_live": int(used),
                     "pool_capacity": int(sum_over_ranks(info["pool_capacity"])),
+                    "pool_capacity_in_run": int(sum_over_ranks(peak_pool)),
                     "mean_probe": round(hs["probe_steps"] / max(1, hs["lookups"]), 3),
                     "max_probe": int(hs["probe_max"]),
                     "kernel_avg_us": round(1e3 * hs["kernel_ms"] / max(1, hs["kernel_launches"]), 2),
                     "hbm_state_bytes": int(sum_over_ranks(hash_bytes)),
                     "dense_hbm_state_bytes": int(sum_over_ranks(dense_bytes)),
                     "state_bytes_note": "hash: table keys + slot->block map + block pool (tsdf/weight/"
-                                        "colour, entry bits, free list) at its grown capacity; dense: "
-                                        "three f32 arrays of the volume"}
+                                        "colour, entry bits, free list) after the run (HashTable.trim; "
+                                        "pool_capacity_in_run: before it, with the growth headroom of the "
+                                        "launches in flight); dense: three f32 arrays of the volume"}
         log(f"[rank {rank}] hash: {Kf / hdt:.0f} frames/s, load {hash_res['load_factor']}, "
             f"pool {info['pool_capacity']} blocks for {info['used']} live")
         ht.close()

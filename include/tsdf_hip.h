@@ -87,6 +87,8 @@ typedef struct {
     int64_t pool_capacity;    /* blocks the pool can hold before it must grow */
     int64_t entries;          /* voxel entries (occupancy bits set), = count_num_hash_entries */
     int64_t slots;            /* slots of the open-addressed device table: the power of two >= capacity */
+    int64_t pool_mapped;      /* 1: the pool lives on reserved address ranges grown by mapping (VMM);
+                                 0: plain allocations grown by copy */
 } tsdf_hash_info_t;
 
 const char* tsdf_last_error(void);
@@ -230,6 +232,10 @@ int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf, float* weight, float* color
  * handle's marching cubes without a host round trip of the volume. */
 int tsdf_hash_to_dense(tsdf_hash_t* h, tsdf_dense_t* d);
 int tsdf_hash_sync(tsdf_hash_t* h);
+/* sync, then a pool on mapped memory hands the memory above its live blocks back (pool_capacity
+ * = live blocks + ~3 %, in whole 32 MB pieces): the end of an asynchronous run, whose growth had
+ * to stay ahead of the launches in flight.  get_volume / get_mesh / export call it. */
+int tsdf_hash_trim(tsdf_hash_t* h);
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);
 

@@ -74,15 +74,20 @@ def test_deferred_hash_per_frame_matches_dense():
     assert h.info()["capacity"] > 37 and h.info()["pool_capacity"] > 16
 
 
-def test_async_hash_overflow_is_reported_not_replayed():
+def test_async_hash_overflow_is_reported_not_replayed(monkeypatch):
     """A pool far too small for asynchronous launches: the skipped bricks cannot be re-run (their
     frames are gone), so the library reports TSDF_E_CAPACITY once, clears the overflow list (no
-    later call replays it against other frames), and the handle works again after reset()."""
+    later call replays it against other frames), and the handle works again after reset().  (The
+    copy-grown pool: a mapped pool grows in 32 MB pieces, which hold this whole extent.)"""
     from tsdf_amd import _ffi, grid_fusion, hash_fusion
+    monkeypatch.setenv("TSDF_HASH_VMM", "0")
     d, c, poses = _synth(24, start=700)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     Tinv = np.linalg.inv(poses)
     h = hash_fusion.HashTable(np.array(BNDS), 0.08, 1 << 12, max_blocks=64)
+    # not a fresh table (whose first asynchronous batch would run synchronously): one synchronous
+    # frame that updates nothing
+    h.integrate_batch(np.zeros_like(d[:1]), c[:1], K, Tinv[:1])
     with pytest.raises(_ffi.TSDFError) as ei:
         h.integrate_batch(d, c, K, Tinv, sync=False)
         h.sync()
@@ -226,3 +231,31 @@ def test_pool_growth_falls_back_whole_when_one_mapping_fails(monkeypatch):
     g.integrate_batch(d, c, K, Tinv)
     for a, b in zip(g.get_state(), h.get_state()):
         assert np.array_equal(a, b)
+
+
+def test_trim_hands_pool_memory_back_and_growth_resumes(monkeypatch):
+    """After an asynchronous run (whose pool growth stays ahead of the launches in flight),
+    HashTable.trim() maps the pool down to its allocated blocks plus ~3 % (whole 32 MB pieces);
+    integration afterwards grows it again, and the state equals the dense grid throughout."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    d, c, poses = _synth(64, start=100)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 16, max_blocks=1 << 12)  # 512^3: 2^18 bricks
+    h.integrate_batch(d[:8], c[:8], K, Tinv[:8])  # synchronous start (reports lag two launches)
+    h.integrate_batch(d[8:40], c[8:40], K, Tinv[8:40], sync=False)
+    h.sync()
+    before = h.info()
+    assert before["pool_mapped"] == 1, before
+    h.trim()
+    after = h.info()
+    per_piece = (32 << 20) // (4 * 512)  # blocks in one 32 MB piece of a state array
+    top = after["blocks_in_pool"]
+    assert after["pool_capacity"] <= before["pool_capacity"]
+    assert top <= after["pool_capacity"] <= top + max(256, top // 32) + per_piece
+    h.integrate_batch(d[40:], c[40:], K, Tinv[40:])
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
+    g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+    assert h.stats()["bricks_skipped"] == 0 or h.info()["pool_capacity"] > after["pool_capacity"]

@@ -1,12 +1,11 @@
 #!/usr/bin/env python3
-"""Voxel-hash load-factor sweep (BASELINE config[2]): the bench's synthetic
-frames into the 512^3 @ 2 cm extent (8^3 blocks) through tables whose capacity puts the final
-load factor at 0.1 .. 0.9 (non-power-of-two capacities; floor-mod home slots like the
-reference), one GPU.  The resize policy is lifted to 0.95 (TSDF_HASH_MAX_LOAD) so the table keeps
-its size.  Per capacity: the insert pass (first pass over the frames, synchronous, every block
-allocated there) and the steady pass (the same frames again: lookups only), frames/s, Mvoxel-updates/s,
-mean / max probe distance, displaced keys.  Also the 1024^3 @ 1 cm extent's cull cost (same
-frames, 2^22 buckets, 8x the bricks the cull walks).  Prints one JSON object.
+"""Voxel-hash load-factor sweep (BASELINE config[2]) on the fused launch: a
+power-of-two device table of 2^18 slots filled to load factors 0.1 .. 0.9 by the blocks of more
+and more frames (the bench ring first, then other camera rings), the resize policy lifted to 0.95
+(TSDF_HASH_MAX_LOAD) so the table keeps its size; at each load the steady pass re-integrates the
+same 64 bench frames (lookups only): frames/s, Mvoxel-updates/s, mean / max probe distance,
+displaced keys.  Also the 1024^3 @ 1 cm extent's cull cost (same frames, 2^22 buckets, 8x the
+bricks the cull walks).  Prints one JSON object.
 
   python tools/hash_sweep.py [--frames 400]
 """
@@ -61,29 +60,67 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             return hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), vs, cap, max_blocks=max_blocks)
 
-    # the scene's live block count at the end of one pass
-    ht = table(0.02, 1 << 22, 64 ** 3)
-    run(ht)
-    live = ht.info()["used"]
-    del ht
-    torch.cuda.empty_cache()
+    # Load factor on the fused launch: a power-of-two device table of S = 2^18 slots (every table
+    # the library builds is one) filled to each target load by the blocks of more and more frames
+    # (the bench ring, then other camera rings), the resize policy lifted; then the steady pass
+    # re-integrates the same 64 bench frames (their blocks exist: lookups only).
+    S = 1 << 18
+    rings = [scene.BENCH_RING, 0.30, 0.20, 0.36, 0.25, 0.12]
+    probe_n = 64
+
+    def ring_frames(rf, n=1000):
+        ps = scene.trajectory(n, seed=0, radius_frac=rf)
+        sp = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
+        dd = torch.empty((n, 480, 640), dtype=torch.int16, device=dev)
+        cc = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
+        for s0 in range(0, n, 50):
+            d, c = scene.render(ps[s0:s0 + 50], sp, seed=0, start=s0, device=dev, depth_dtype=torch.int16)
+            dd[s0:s0 + len(d)] = d
+            cc[s0:s0 + len(c)] = c
+        return dd, cc, np.ascontiguousarray(np.linalg.inv(ps))
+
+    ring_data = [(depth, rgb, Tinv)] + [None] * (len(rings) - 1)
+
+    def chunk(ht, r, f0, n, sync=True):
+        if ring_data[r] is None:
+            ring_data[r] = ring_frames(rings[r])
+        dd, cc, T = ring_data[r]
+        n = min(n, dd.shape[0] - f0)
+        ht.integrate_batch(dd[f0].data_ptr(), cc[f0].data_ptr(), K, T[f0:f0 + n], hw=(480, 640),
+                           device_ptrs=True, sync=sync)
+        return n
+
     out = []
     for lf in [float(x) for x in a.loads.split(",")]:
-        cap = int(math.ceil(live / lf))
-        ht = table(0.02, cap, 64 ** 3)
-        r = {"target_load": lf, "capacity": cap}
-        # the insert pass is synchronous (the resize policy alone decides the table size: the
-        # asynchronous growth headroom would resize it early); the steady pass is asynchronous
-        for name, sync in (("insert_pass", True), ("steady_pass", False)):
-            dt, st = run(ht, sync)
-            info = ht.info()
-            r[name] = {"frames_per_s": round(F / dt, 1), "mvox_updates_per_s": round(st["voxel_updates"] / dt / 1e6, 1),
-                       "mean_probe": round(st["probe_steps"] / max(1, st["lookups"]), 3),
-                       "max_probe": int(st["probe_max"]), "blocks_allocated": int(st["blocks_allocated"])}
-        r.update({"load_factor": round(info["used"] / info["capacity"], 4), "displaced": int(info["displaced"]),
-                  "blocks_live": int(info["used"]), "capacity_final": int(info["capacity"])})
-        print(json.dumps(r), file=sys.stderr, flush=True)
-        out.append(r)
+        ht = table(0.02, S, 64 ** 3)
+        chunk(ht, 0, 0, probe_n)
+        r, f = 0, probe_n
+        while ht.info()["used"] < lf * S and r < len(rings):
+            n = chunk(ht, r, f, 64)
+            f += n
+            if n == 0 or f >= 1000:
+                r, f = r + 1, 0
+        info = ht.info()
+        res = {"target_load": lf, "slots": int(info["slots"]), "blocks_live": int(info["used"]),
+               "load_factor": round(info["used"] / info["slots"], 4), "displaced": int(info["displaced"]),
+               "max_probe_in_table": int(info["max_probe"])}
+        ht.stats(reset=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = 4
+        for _ in range(reps):
+            chunk(ht, 0, 0, probe_n, sync=False)
+        ht.sync()
+        dt = time.perf_counter() - t0
+        st = ht.stats()
+        if st["bricks_skipped"]:
+            raise RuntimeError("bricks skipped")
+        res["steady_pass"] = {"frames_per_s": round(reps * probe_n / dt, 1),
+                              "mvox_updates_per_s": round(st["voxel_updates"] / dt / 1e6, 1),
+                              "mean_probe": round(st["probe_steps"] / max(1, st["lookups"]), 3),
+                              "max_probe": int(st["probe_max"])}
+        print(json.dumps(res), file=sys.stderr, flush=True)
+        out.append(res)
         del ht
         torch.cuda.empty_cache()
     # 1024^3 @ 1 cm extent (config[4]'s): the cull walks 2^21 bricks per batch
@@ -100,8 +137,9 @@ def main():
         print(json.dumps(ext), file=sys.stderr, flush=True)
         del ht
         torch.cuda.empty_cache()
-    print(json.dumps({"sweep": out, "frames": F, "live_blocks": live, "extent_cost": ext,
-                      "volume": "512^3 @ 2 cm extent, 8^3 blocks, bench ring frames"}))
+    print(json.dumps({"sweep": out, "frames": F, "slots": S, "extent_cost": ext,
+                      "volume": "512^3 @ 2 cm extent, 8^3 blocks; steady pass = the first 64 bench-ring frames x 4",
+                      "kernel": "k_fused_hash<0> (power-of-two device table, z-half waves)"}))
 
 
 if __name__ == "__main__":

@@ -9,6 +9,7 @@
 // free list.  A voxel "entry" (count_num_hash_entries, get_hash_entry) is one bit of the
 // block's 512-bit occupancy mask, set by integrate or by an explicit insert.
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -53,11 +54,25 @@ struct VArray {
         base = (char*)b;
         return true;
     }
-    int grow(size_t bytes) {  // map [mapped, round_up(bytes))
+    // Map [mapped, round_up(bytes)) in pieces of at most kPiece bytes, so that trim() can hand
+    // whole pieces back at the top later.
+    static constexpr size_t kPiece = 32ull << 20;
+    int grow(size_t bytes) {
         const size_t want = (bytes + gran - 1) / gran * gran;
-        if (want <= mapped) return TSDF_OK;
         if (want > reserved) return set_error(TSDF_E_CAPACITY, "pool beyond its reservation");
-        const size_t sz = want - mapped;
+        const size_t piece = std::max(gran, kPiece / gran * gran);
+        while (mapped < want) TSDF_TRY(map_piece(std::min(piece, want - mapped)));
+        return TSDF_OK;
+    }
+    // Unmap whole pieces above `bytes` (nothing may address them: the caller drained the stream).
+    void trim(size_t bytes) {
+        const size_t keep = (bytes + gran - 1) / gran * gran;
+        size_t n = chunks.size();
+        size_t top = mapped;
+        while (n > 0 && top - chunks[n - 1].second >= keep) top -= chunks[--n].second;
+        unmap_to(n);
+    }
+    int map_piece(size_t sz) {
         const hipMemAllocationProp p = prop();
         hipMemGenericAllocationHandle_t hdl;
         hipError_t e = hipMemCreate(&hdl, sz, &p, 0);
@@ -78,7 +93,7 @@ struct VArray {
                              hipGetErrorString(e));
         }
         chunks.emplace_back(hdl, sz);
-        mapped = want;
+        mapped += sz;
         return TSDF_OK;
     }
     // undo the mappings made after the array held `n_chunks` chunks (a failed multi-array growth)
@@ -137,8 +152,9 @@ struct tsdf_hash {
     long long rb_used = -1;       // live blocks in the last report read (or at the last sync check)
     long long deltas[4] = {};     // growth of live blocks over the last four reports / checks
     int n_delta = 0;
-    void note_live(long long used) {  // a new live-block count: remember its growth
-        if (rb_used >= 0 && used > rb_used) deltas[n_delta++ & 3] = used - rb_used;
+    void note_live(long long used) {  // a new live-block count: remember its growth (from 0 at first)
+        const long long prev = rb_used < 0 ? 0 : rb_used;
+        if (used > prev) deltas[n_delta++ & 3] = used - prev;
         rb_used = used;
     }
     long long recent_growth() const {  // the largest of the recent growths (at least 256 blocks)
@@ -153,6 +169,13 @@ struct tsdf_hash {
     bool vmm = false;
     VArray va[5];
     int vmm_fail_at = -1;  // test hook (TSDF_HASH_VMM_FAIL=k): the next growth of array k fails
+    static constexpr size_t kPer[5] = {sizeof(float) * kBrickVox, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
+                                       sizeof(unsigned long long) * 8, sizeof(int)};
+    long long mapped_blocks() const {  // blocks every pool array has memory for
+        long long n = LLONG_MAX;
+        for (int k = 0; k < 5; ++k) n = std::min<long long>(n, (long long)(va[k].mapped / kPer[k]));
+        return n;
+    }
     // Back blocks [0, n) of every pool array, all or nothing: if one array cannot grow, the
     // arrays grown before it are unmapped back to their old size, so the pool stays consistent
     // for the copy fallback (grow_pool).
@@ -169,8 +192,8 @@ struct tsdf_hash {
             } else {
                 r = va[k].grow(per[k] * (size_t)n);
             }
-            if (r != TSDF_OK) {
-                for (int j = 0; j < k; ++j) va[j].unmap_to(before[j]);
+            if (r != TSDF_OK) {  // (array k may hold some of its new pieces too)
+                for (int j = 0; j <= k; ++j) va[j].unmap_to(before[j]);
                 return r;
             }
         }
@@ -549,7 +572,7 @@ int grow_pool(tsdf_hash* h, long long new_max) {
     if (new_max <= t.max_blocks) return TSDF_OK;
     if (h->vmm) {  // map more physical memory behind the reserved ranges: no copy, no drain
         if (h->map_pool(new_max) == TSDF_OK) {
-            t.max_blocks = new_max;
+            t.max_blocks = std::min<long long>(h->mapped_blocks(), B.n_bricks);  // (whole pieces)
             return TSDF_OK;
         }
         // mapping refused: continue with plain allocations (copy below, then unmap the ranges)
@@ -588,6 +611,21 @@ int grow_pool(tsdf_hash* h, long long new_max) {
     t.occ = no;
     t.free_list = nf;
     t.max_blocks = new_max;
+    return TSDF_OK;
+}
+
+// Hand mapped pool memory above the bump pointer back (VMM pools only, at a sync point: nothing is
+// in flight): the pool keeps pool_top + 1/32 of it (at least 256 blocks) rounded up to whole
+// pieces, so after an asynchronous run -- whose growth had to stay ahead of the launches in
+// flight -- the pool holds about the live blocks again.
+int trim_pool(tsdf_hash* h) {
+    if (!h->vmm) return TSDF_OK;
+    TSDF_TRY(read_state(h));
+    const long long top = h->host_st.pool_top;
+    const long long keep = std::max<long long>(top + std::max<long long>(256, top / 32), 64);
+    if (keep >= h->t.max_blocks) return TSDF_OK;
+    for (int k = 0; k < 5; ++k) h->va[k].trim(tsdf_hash::kPer[k] * (size_t)keep);
+    h->t.max_blocks = std::min<long long>(h->mapped_blocks(), h->b.n_bricks);
     return TSDF_OK;
 }
 
@@ -868,6 +906,16 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_HIP(hipSetDevice(B.device));
     const unsigned cull_grid = B.cull_grid();
     const bool sync = !(flags & TSDF_ASYNC);
+    if (!sync && h->rb_used < 0 && n_frames > kMaxBatch && B.prestaged < 0) {
+        // A fresh table's first asynchronous call: its first batch runs synchronously (the pool
+        // grows exactly and skipped bricks re-run), so the growth of the batches in flight is
+        // known before any launch depends on a lagging report.
+        TSDF_TRY(hash_run(h, kMaxBatch, depth, dk, color, ck, H, W, K, Tinv, flags & ~TSDF_ASYNC));
+        depth = (const char*)depth + frame_bytes_depth(dk, H, W) * kMaxBatch;
+        color = (const char*)color + frame_bytes_color(ck, H, W) * kMaxBatch;
+        Tinv += 16 * kMaxBatch;
+        n_frames -= kMaxBatch;
+    }
     if (sync && h->async_pending) TSDF_TRY(take_overflow(h));  // before any replay of this call
     if (!sync) h->async_pending = true;
     TSDF_TRY(B.begin_call(depth, frame_bytes_depth(dk, H, W) * n_frames, color,
@@ -1299,6 +1347,7 @@ int tsdf_hash_info(tsdf_hash_t* h, tsdf_hash_info_t* out) {
     TSDF_TRY(read_state(h));
     out->capacity = h->map_size;
     out->slots = h->t.capacity;
+    out->pool_mapped = h->vmm ? 1 : 0;
     out->used = (int64_t)inf.used;
     out->tombstones = (int64_t)inf.tomb;
     out->displaced = (int64_t)inf.displaced;
@@ -1358,6 +1407,12 @@ int tsdf_hash_sync(tsdf_hash_t* h) {
     TSDF_HIP(hipStreamSynchronize(h->b.stream));
     if (h->async_pending) TSDF_TRY(take_overflow(h));
     return TSDF_OK;
+}
+
+int tsdf_hash_trim(tsdf_hash_t* h) {
+    if (!h) return set_error(TSDF_E_ARG, "null handle");
+    TSDF_TRY(tsdf_hash_sync(h));
+    return trim_pool(h);
 }
 
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset) {

@@ -52,7 +52,8 @@ class HashInfo(ctypes.Structure):
     _fields_ = [("capacity", ctypes.c_int64), ("used", ctypes.c_int64),
                 ("tombstones", ctypes.c_int64), ("displaced", ctypes.c_int64),
                 ("max_probe", ctypes.c_int64), ("blocks_in_pool", ctypes.c_int64),
-                ("pool_capacity", ctypes.c_int64), ("entries", ctypes.c_int64), ("slots", ctypes.c_int64)]
+                ("pool_capacity", ctypes.c_int64), ("entries", ctypes.c_int64), ("slots", ctypes.c_int64),
+                ("pool_mapped", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -97,6 +98,7 @@ SIGNATURES = {
     "tsdf_hash_info": [_P, _P],
     "tsdf_hash_get_dense": [_P, _P, _P, _P],
     "tsdf_hash_to_dense": [_P, _P],
+    "tsdf_hash_trim": [_P],
     "tsdf_hash_export_blocks": [_P, _P, _P, _P, _P, _P, _P, _I],
     "tsdf_hash_import_blocks": [_P, _P, _I64, _P, _P, _P, _P, _I],
     "tsdf_hash_sync": [_P],
