@@ -233,8 +233,9 @@ int tsdf_hash_get_dense(tsdf_hash_t* h, float* tsdf, float* weight, float* color
 int tsdf_hash_to_dense(tsdf_hash_t* h, tsdf_dense_t* d);
 int tsdf_hash_sync(tsdf_hash_t* h);
 /* sync, then a pool on mapped memory hands the memory above its live blocks back (pool_capacity
- * = live blocks + ~3 %, in whole 32 MB pieces): the end of an asynchronous run, whose growth had
- * to stay ahead of the launches in flight.  get_volume / get_mesh / export call it. */
+ * = live blocks + ~3 %, in whole 8 MB pieces; the live blocks move into fresh mapped ranges by one
+ * device copy): the end of an asynchronous run, whose growth had to stay ahead of the launches in
+ * flight.  get_volume / get_mesh call it.  Not in the reference (its pool is a Python dict). */
 int tsdf_hash_trim(tsdf_hash_t* h);
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);

@@ -115,7 +115,8 @@ def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe, vmm):
     d, c, poses = _synth(72, start=100)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     Tinv = np.linalg.inv(poses)
-    h = hash_fusion.HashTable(np.array(BNDS), 0.04, 1 << 12, max_blocks=256)  # 256^3: 8.2k blocks by the end
+    # 512^3: ~56k blocks by the end, many pool pieces (4096 blocks each) past the first batch's
+    h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 12, max_blocks=256)
     h.integrate_batch(d[:8], c[:8], K, Tinv[:8])  # synchronous start
     cap0 = h.info()["pool_capacity"]
     skipped0 = h.stats()["bricks_skipped"]
@@ -124,7 +125,7 @@ def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe, vmm):
     assert h.stats()["bricks_skipped"] == skipped0
     info = h.info()
     assert info["pool_capacity"] > cap0 and info["capacity"] > 1 << 12
-    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.04)
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
     g.integrate_batch(d, c, K, Tinv)
     for a, b in zip(g.get_state(), h.get_state()):
         assert np.array_equal(a, b)
@@ -235,7 +236,8 @@ def test_pool_growth_falls_back_whole_when_one_mapping_fails(monkeypatch):
 
 def test_trim_hands_pool_memory_back_and_growth_resumes(monkeypatch):
     """After an asynchronous run (whose pool growth stays ahead of the launches in flight),
-    HashTable.trim() maps the pool down to its allocated blocks plus ~3 % (whole 32 MB pieces);
+    HashTable.trim() compacts the pool into fresh mapped ranges of its allocated blocks plus ~3 %
+    (whole 8 MB pieces);
     integration afterwards grows it again, and the state equals the dense grid throughout."""
     from tsdf_amd import grid_fusion, hash_fusion
     d, c, poses = _synth(64, start=100)
@@ -249,7 +251,7 @@ def test_trim_hands_pool_memory_back_and_growth_resumes(monkeypatch):
     assert before["pool_mapped"] == 1, before
     h.trim()
     after = h.info()
-    per_piece = (32 << 20) // (4 * 512)  # blocks in one 32 MB piece of a state array
+    per_piece = (8 << 20) // (4 * 512)  # blocks in one 8 MB piece of a state array
     top = after["blocks_in_pool"]
     assert after["pool_capacity"] <= before["pool_capacity"]
     assert top <= after["pool_capacity"] <= top + max(256, top // 32) + per_piece

@@ -45,32 +45,31 @@ struct VArray {
             (void)hipGetLastError();  // leave no sticky error behind
             return false;
         }
-        reserved = (max_bytes + gran - 1) / gran * gran;
+        piece = std::max(gran, kPiece / gran * gran);
+        reserved = (max_bytes + piece - 1) / piece * piece;
         void* b = nullptr;
-        if (hipMemAddressReserve(&b, reserved, gran, nullptr, 0) != hipSuccess) {
+        if (hipMemAddressReserve(&b, reserved, std::max<size_t>(gran, 2u << 20), nullptr, 0) != hipSuccess) {
             (void)hipGetLastError();
             return false;
         }
         base = (char*)b;
         return true;
     }
-    // Map [mapped, round_up(bytes)) in pieces of at most kPiece bytes, so that trim() can hand
-    // whole pieces back at the top later.
-    static constexpr size_t kPiece = 32ull << 20;
+    // Map [mapped, round_up(bytes)) in pieces of one size.  One size for every piece of an array:
+    // on this ROCm a piece whose size differs from the one mapped before it is refused by
+    // hipMemSetAccess ("invalid argument"), while equal pieces map at any count
+    // (tools/gpu/vmm_probe.hip).  Pieces are only unmapped at release or to undo a failed growth
+    // (pieces no kernel has used): an address range that kernels have written is never unmapped
+    // and mapped again -- measured on the box, a piece mapped where a used one had been unmapped
+    // lost the writes of one 2 MB fragment to a stale translation (tools/gpu/vmm_diag.py), so the
+    // pool hands memory back by compaction into fresh ranges (trim_pool).
+    static constexpr size_t kPiece = 8ull << 20;
+    size_t piece = 0;
     int grow(size_t bytes) {
-        const size_t want = (bytes + gran - 1) / gran * gran;
+        const size_t want = (bytes + piece - 1) / piece * piece;
         if (want > reserved) return set_error(TSDF_E_CAPACITY, "pool beyond its reservation");
-        const size_t piece = std::max(gran, kPiece / gran * gran);
-        while (mapped < want) TSDF_TRY(map_piece(std::min(piece, want - mapped)));
+        while (mapped < want) TSDF_TRY(map_piece(piece));
         return TSDF_OK;
-    }
-    // Unmap whole pieces above `bytes` (nothing may address them: the caller drained the stream).
-    void trim(size_t bytes) {
-        const size_t keep = (bytes + gran - 1) / gran * gran;
-        size_t n = chunks.size();
-        size_t top = mapped;
-        while (n > 0 && top - chunks[n - 1].second >= keep) top -= chunks[--n].second;
-        unmap_to(n);
     }
     int map_piece(size_t sz) {
         const hipMemAllocationProp p = prop();
@@ -615,16 +614,45 @@ int grow_pool(tsdf_hash* h, long long new_max) {
 }
 
 // Hand mapped pool memory above the bump pointer back (VMM pools only, at a sync point: nothing is
-// in flight): the pool keeps pool_top + 1/32 of it (at least 256 blocks) rounded up to whole
-// pieces, so after an asynchronous run -- whose growth had to stay ahead of the launches in
-// flight -- the pool holds about the live blocks again.
+// in flight): the blocks [0, pool_top) and the free list move into fresh reserved ranges mapped for
+// pool_top + 1/32 of it (at least 256 blocks), rounded up to whole pieces, and the old ranges are
+// released -- so after an asynchronous run, whose growth had to stay ahead of the launches in
+// flight, the pool holds about the live blocks again.  A compaction, not an unmap of the top
+// pieces: see VArray::grow.  One device copy of the live state (~1.1 GB at 512^3: ~0.5 ms).
+// Nothing changes when the new ranges cannot be had.
 int trim_pool(tsdf_hash* h) {
     if (!h->vmm) return TSDF_OK;
     TSDF_TRY(read_state(h));
     const long long top = h->host_st.pool_top;
     const long long keep = std::max<long long>(top + std::max<long long>(256, top / 32), 64);
-    if (keep >= h->t.max_blocks) return TSDF_OK;
-    for (int k = 0; k < 5; ++k) h->va[k].trim(tsdf_hash::kPer[k] * (size_t)keep);
+    if (keep + (long long)(VArray::kPiece / tsdf_hash::kPer[0]) > h->t.max_blocks) return TSDF_OK;  // < one piece to gain
+    const size_t nb = (size_t)h->b.n_bricks;
+    VArray nv[5];
+    bool ok = true;
+    for (int k = 0; k < 5 && ok; ++k)
+        ok = nv[k].reserve(h->b.device, tsdf_hash::kPer[k] * nb) && nv[k].grow(tsdf_hash::kPer[k] * (size_t)keep) == TSDF_OK;
+    if (ok) {
+        const long long n = std::min<long long>(keep, h->t.max_blocks);  // (>= pool_top, >= free_count)
+        for (int k = 0; k < 5 && ok; ++k)
+            ok = hipMemcpyAsync(nv[k].base, h->va[k].base, tsdf_hash::kPer[k] * (size_t)n, hipMemcpyDeviceToDevice,
+                                h->b.stream) == hipSuccess;
+        ok = ok && hipStreamSynchronize(h->b.stream) == hipSuccess;
+    }
+    if (!ok) {  // keep the pool as it is
+        (void)hipGetLastError();
+        for (auto& v : nv) v.release();
+        return TSDF_OK;
+    }
+    for (int k = 0; k < 5; ++k) {
+        h->va[k].release();
+        h->va[k] = nv[k];
+        nv[k] = VArray{};
+    }
+    h->b.pool.tsdf = (float*)h->va[0].base;
+    h->b.pool.weight = (float*)h->va[1].base;
+    h->b.pool.color = (float*)h->va[2].base;
+    h->t.occ = (unsigned long long*)h->va[3].base;
+    h->t.free_list = (int*)h->va[4].base;
     h->t.max_blocks = std::min<long long>(h->mapped_blocks(), h->b.n_bricks);
     return TSDF_OK;
 }
