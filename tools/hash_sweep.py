@@ -86,6 +86,8 @@ def main():
             ring_data[r] = ring_frames(rings[r])
         dd, cc, T = ring_data[r]
         n = min(n, dd.shape[0] - f0)
+        if n <= 0:
+            return 0
         ht.integrate_batch(dd[f0].data_ptr(), cc[f0].data_ptr(), K, T[f0:f0 + n], hw=(480, 640),
                            device_ptrs=True, sync=sync)
         return n

@@ -536,3 +536,12 @@ int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {
 }
 
 }  // extern "C"
+
+#ifdef TSDF_WG_TIMES
+// (diagnostic builds) the last fused launch's per-workgroup start / end / items: out[3 * 8192]
+extern "C" int tsdf_diag_wg_times(unsigned long long* out) {
+    TSDF_HIP(hipDeviceSynchronize());
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 3 * 8192));
+    return TSDF_OK;
+}
+#endif

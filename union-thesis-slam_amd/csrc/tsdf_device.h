@@ -1410,6 +1410,11 @@ struct Stage {
     int* res_c;
 };
 
+#ifdef TSDF_WG_TIMES
+// Diagnostic builds only (tools/gpu/wg_times.py): per integrate workgroup of the last fused launch,
+// its start and end (s_memrealtime, 100 MHz) and the list items its waves took.
+__device__ unsigned long long g_wg_times[3][8192];
+#endif
 template <bool OW1, int NZ, int DK = 0>
 __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_DENSE_WAVES))) void k_fused(Vol v, Batch bi, Batch bc, Batch bp,
                                                                      Pool pool, unsigned long long* stats,
@@ -1421,6 +1426,9 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     const int tid = threadIdx.x, b = blockIdx.x;
     const Table no_table{};
     if (b < sg.gi) {
+#ifdef TSDF_WG_TIMES
+        if (tid == 0 && b < 8192) g_wg_times[0][b] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (tid < kNStat) s_stat[tid] = 0;
         if (tid == 0) s_next = 0;
         if (OW1)
@@ -1431,6 +1439,12 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
                                              OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
         __syncthreads();
+#ifdef TSDF_WG_TIMES
+        if (tid == 0 && b < 8192) {
+            g_wg_times[1][b] = __builtin_amdgcn_s_memrealtime();
+            g_wg_times[2][b] = s_next;
+        }
+#endif
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
         cull_superbrick<false>(v, bc, no_table, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
