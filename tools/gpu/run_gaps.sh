@@ -1,0 +1,11 @@
+# Launch gaps of the fused dense launch: rocprofv3 kernel trace of rank 0 of 8 and of one GPU
+# (scaling_sim --only), the trace CSV copied to gpurun_out/gaps/ (tools/launch_gaps.py reads it).
+set -o pipefail
+R=$(pwd)
+O=$R/gpurun_out/gaps
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for w in 8 1; do
+  timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/gap_$w -o run --output-format csv -- python "$R/tools/scaling_sim.py" --only $w:0 --steps 400 --warmup 48 > $O/w$w.json 2> $O/w$w.err || exit $?
+  find /tmp/gap_$w -name "*kernel_trace.csv" -exec cp {} $O/trace_w$w.csv \;
+done

@@ -1,5 +1,5 @@
-"""Where the time of an eighth-shard launch goes: per integrate workgroup of the last fused launch
-of a call, its start, end and list items (diagnostic build: tools/build_variant.sh wgt
+"""Where the time of an eighth-shard launch goes: per workgroup of the last fused launch of a call
+(integrate, cull and prep roles), its start, end and list items (diagnostic build: tools/build_variant.sh wgt
 "-DTSDF_WG_TIMES", run with TSDF_HIP_LIB=abtest/libwgt.so).  Bench workload (scaling_sim's), one
 GPU and rank 0 of 2 / 4 / 8 cyclic column shards.  Prints one JSON line per configuration."""
 import ctypes
@@ -33,39 +33,48 @@ def main():
     lib = _ffi.load()
     fn = lib.tsdf_diag_wg_times
     fn.argtypes = [ctypes.c_void_p]
-    buf = np.zeros((3, 8192), np.uint64)
+    NW = 16384
+    buf = np.zeros((3, NW), np.uint64)
     for world in (1, 2, 4, 8):
         vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(0, world))
         rows = []
-        for start in range(0, 192, 8):
-            vol.integrate_batch(depth.data_ptr() + start * ds, rgb.data_ptr() + start * cs, K, Tinv[start:start + 8],
+        for start in range(0, 192, 32):  # 4 batches a call: its launch 1 runs all three stages
+            vol.integrate_batch(depth.data_ptr() + start * ds, rgb.data_ptr() + start * cs, K, Tinv[start:start + 32],
                                 hw=(480, 640), device_ptrs=True)
-            if start < 48:
+            if start < 64:
                 continue
             fn(buf.ctypes.data)
-            n = int(np.count_nonzero(buf[1]))
-            t0 = buf[0, :n].astype(np.int64)
-            t1 = buf[1, :n].astype(np.int64)
-            it = buf[2, :n].astype(np.int64)
+            t0 = buf[0].astype(np.int64)
+            keep = (buf[1] != 0) & (t0 > t0.max() - 100000)  # this launch only (not an older, larger one)
+            t0 = t0[keep]
+            t1 = buf[1][keep].astype(np.int64)
+            role = (buf[2][keep] >> np.uint64(32)).astype(np.int64)
+            it = (buf[2][keep] & np.uint64(0xFFFFFFFF)).astype(np.int64)
             base = t0.min()
-            s, e = (t0 - base) / 100.0, (t1 - base) / 100.0  # us
-            rows.append([e.max(), np.median(e), np.percentile(e, 10), s.max(), (e - s).mean(), it.mean(), it.min(), it.max()])
-        r = np.array(rows).mean(axis=0)
-        if os.environ.get("WG_DUMP") and world in (1, 8):
-            busy = (t1 - t0) / 100.0
-            by_xcd = [round(float(busy[x::8].mean()), 1) for x in range(8)]
-            pair = busy[:256] - busy[256:512] if n >= 512 else busy[:0]
-            print(json.dumps({"world": world, "busy_by_xcd": by_xcd,
-                              "busy_first_half": round(float(busy[:256].mean()), 1),
-                              "busy_second_half": round(float(busy[256:].mean()), 1),
-                              "items_corr": round(float(np.corrcoef(busy, it)[0, 1]), 3),
-                              "pair_diff_std": round(float(pair.std()), 1) if len(pair) else None,
-                              "busy_sorted_deciles": [round(float(x), 1) for x in np.percentile(busy, range(0, 101, 10))],
-                              "busy_first32": [round(float(x), 1) for x in busy[:32]]}), flush=True)
-        print(json.dumps({"world": world, "wgs": n, "span_us": round(r[0], 2), "end_median_us": round(r[1], 2),
-                          "end_p10_us": round(r[2], 2), "last_start_us": round(r[3], 2),
-                          "wg_busy_mean_us": round(r[4], 2), "items_mean": round(r[5], 1),
-                          "items_min": int(r[6]), "items_max": int(r[7])}), flush=True)
+            s, e = (t0 - base) / 100.0, (t1 - base) / 100.0  # us from the first workgroup's start
+            r = {"span": e.max()}
+            for code, name in ((0, "integrate"), (1, "cull"), (2, "prep")):
+                m = role == code
+                if not m.any():
+                    continue
+                r[name] = [int(m.sum()), s[m].min(), s[m].max(), np.median(e[m]), e[m].max(), (e[m] - s[m]).mean()]
+            r["items"] = it[role == 0]
+            r["busy"] = (e - s)[role == 0]
+            rows.append(r)
+        out = {"world": world, "span_us": round(float(np.mean([r["span"] for r in rows])), 2)}
+        for name in ("integrate", "cull", "prep"):
+            v = np.array([r[name] for r in rows if name in r])
+            if len(v):
+                out[name] = {"wgs": int(v[0, 0]), "first_start_us": round(float(v[:, 1].mean()), 2),
+                             "last_start_us": round(float(v[:, 2].mean()), 2),
+                             "end_median_us": round(float(v[:, 3].mean()), 2),
+                             "last_end_us": round(float(v[:, 4].mean()), 2),
+                             "busy_mean_us": round(float(v[:, 5].mean()), 2)}
+        it = np.concatenate([r["items"] for r in rows])
+        out["integrate"]["items_mean"] = round(float(it.mean()), 1)
+        busy = rows[-1]["busy"]
+        out["integrate"]["busy_deciles_last"] = [round(float(x), 1) for x in np.percentile(busy, range(0, 101, 10))]
+        print(json.dumps(out), flush=True)
         del vol
 
 

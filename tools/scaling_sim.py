@@ -123,7 +123,9 @@ def hash_shards(a, timed, bnds):
             timed(ht, 0, a.warmup)
             ht.stats(reset=True)
             t = timed(ht, a.warmup, a.steps)
-            st, info = ht.stats(), ht.info()
+            st = ht.stats()
+            ht.trim()  # the pool at its live blocks (the run's growth headroom handed back)
+            info = ht.info()
             state = info["slots"] * 12 + info["pool_capacity"] * per_block
             res.append({"rank": r, "fps": round(a.steps / t, 1),
                         "mvox_updates_per_s": round(st["voxel_updates"] / t / 1e6, 1),

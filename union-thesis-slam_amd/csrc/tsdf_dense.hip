@@ -14,6 +14,7 @@ struct tsdf_dense {
     Mesh mesh;
     int nz = 4;  // z-steps per wave in k_integrate (8: a brick per wave; 4: a z-half per wave)
     bool fused = true;  // three-stage pipeline launches (k_fused) when a call allows them
+    int gi_per_cu = 0;  // integrate workgroups per CU in a fused launch (0: as many as fit)
 };
 
 namespace {
@@ -114,8 +115,9 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
     Base& B = h->b;
     TSDF_TRY(B.use_sets(kSets));
     const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
-    const int gi_full = h->nz == 4 ? (int)B.grid_for((const void*)k_fused<true, 4>, kFusedWG)
-                                   : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
+    const int gi_occ = h->nz == 4 ? (int)B.grid_for((const void*)k_fused<true, 4>, kFusedWG)
+                                  : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
+    const int gi_full = h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ;
     const int gc_full = (int)B.cull_grid();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
@@ -289,6 +291,7 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
     if (r == TSDF_OK) {
         // three-stage pipeline launches; TSDF_PIPELINE=0 forces the in-line path
         if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;
+        if (const char* e = getenv("TSDF_FUSED_GI_PER_CU")) h->gi_per_cu = std::max(0, atoi(e));  // A/B override
     }
     if (r == TSDF_OK) {
         const size_t n = (size_t)h->b.n_bricks * kBrickVox * sizeof(float);
@@ -538,10 +541,11 @@ int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {
 }  // extern "C"
 
 #ifdef TSDF_WG_TIMES
-// (diagnostic builds) the last fused launch's per-workgroup start / end / items: out[3 * 8192]
+// (diagnostic builds) the last fused launch's per-workgroup start / end / role|items:
+// out[3 * kWgTimes]
 extern "C" int tsdf_diag_wg_times(unsigned long long* out) {
     TSDF_HIP(hipDeviceSynchronize());
-    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 3 * 8192));
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 3 * kWgTimes));
     return TSDF_OK;
 }
 #endif

@@ -1128,6 +1128,15 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, Li
 // grid, all resident), so the work is spread evenly whatever the frames see.  `count` (device)
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
+#ifndef TSDF_PRIO  // progress priority of the dense integrate's waves (integrate_items)
+#define TSDF_PRIO 0
+#endif
+#ifndef TSDF_PRIO_HASH  // ... and of the hash integrate's
+#define TSDF_PRIO_HASH 1
+#endif
+#ifndef TSDF_PRIO_MIN  // ... for workgroups with at least this many list items (brick parts)
+#define TSDF_PRIO_MIN 64
+#endif
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
@@ -1175,10 +1184,33 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // the workgroup's waves from an LDS counter: a wave that
         // drew short items takes more, so a workgroup ends when its last item does, not when its
         // unluckiest wave's static share does (the tail of small shards: few items per wave).
+        // Progress priority (hash launches): the SIMDs arbitrate VALU issue by priority, then age,
+        // so of the workgroups sharing a CU the first-dispatched one runs ahead and the last runs
+        // its tail alone.  A wave's priority falls as its workgroup's share is taken (3 below 1/2,
+        // 2 below 13/16, 1 below 15/16, then 0), so a workgroup that lags keeps the issue slots
+        // until it has caught up.  Hash: +4 % on one GPU (z-half waves that wait for their
+        // partner's claim word stop losing the SIMD to older workgroups), but -5 % on an eighth
+        // shard (~15 items per workgroup), so only for workgroups with many items; dense: neutral
+        // on one GPU, -2 % on an eighth shard, so off.
+        constexpr bool kPrio = HASH ? TSDF_PRIO_HASH != 0 : TSDF_PRIO != 0;
+        const unsigned mine = total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
+        const bool use_prio = kPrio && mine >= TSDF_PRIO_MIN;  // (wave-uniform)
+        [[maybe_unused]] int prio = 3;
+        if (use_prio) __builtin_amdgcn_s_setprio(3);
         for (;;) {
             unsigned j = 0;
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
+            if (use_prio) {
+                const unsigned q = j * 16u;
+                const int p = q < mine * 8u ? 3 : q < mine * 13u ? 2 : q < mine * 15u ? 1 : 0;
+                if (p != prio) {
+                    prio = p;
+                    if (p == 2) __builtin_amdgcn_s_setprio(2);
+                    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+            }
             // bricks dealt to workgroups (brick k to workgroup k mod n_wg), the parts of one brick
             // taken one after the other, so they run side by side on the workgroup's waves and
             // share their depth / colour gathers in the CU's cache
@@ -1189,6 +1221,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
                                                    (int)(j % parts) * NZ, s_stat, s_rcp, nupd, res);
         }
+        if (use_prio) __builtin_amdgcn_s_setprio(0);
         return;
     }
     for (int e = wave; e < total * parts; e += n_waves) {
@@ -1411,9 +1444,11 @@ struct Stage {
 };
 
 #ifdef TSDF_WG_TIMES
-// Diagnostic builds only (tools/gpu/wg_times.py): per integrate workgroup of the last fused launch,
-// its start and end (s_memrealtime, 100 MHz) and the list items its waves took.
-__device__ unsigned long long g_wg_times[3][8192];
+// Diagnostic builds only (tools/gpu/wg_times.py): per workgroup of the last full fused launch, its
+// start and end (s_memrealtime, 100 MHz) and role << 32 | the list items its waves took (role 0
+// integrate, 1 cull, 2 prep).
+constexpr int kWgTimes = 16384;
+__device__ unsigned long long g_wg_times[3][kWgTimes];
 #endif
 template <bool OW1, int NZ, int DK = 0>
 __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_DENSE_WAVES))) void k_fused(Vol v, Batch bi, Batch bc, Batch bp,
@@ -1425,10 +1460,12 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     __shared__ unsigned s_next;
     const int tid = threadIdx.x, b = blockIdx.x;
     const Table no_table{};
-    if (b < sg.gi) {
 #ifdef TSDF_WG_TIMES
-        if (tid == 0 && b < 8192) g_wg_times[0][b] = __builtin_amdgcn_s_memrealtime();
+    // (launches with all three stages only: the steady state of a call)
+    const bool rec = sg.gi > 0 && sg.gc > 0 && (int)gridDim.x > sg.gi + sg.gc && b < kWgTimes;
+    if (tid == 0 && rec) g_wg_times[0][b] = __builtin_amdgcn_s_memrealtime();
 #endif
+    if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
         if (tid == 0) s_next = 0;
         if (OW1)
@@ -1439,12 +1476,6 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
                                              OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
         __syncthreads();
-#ifdef TSDF_WG_TIMES
-        if (tid == 0 && b < 8192) {
-            g_wg_times[1][b] = __builtin_amdgcn_s_memrealtime();
-            g_wg_times[2][b] = s_next;
-        }
-#endif
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
         cull_superbrick<false>(v, bc, no_table, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
@@ -1455,6 +1486,14 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
         float(*sa)[33] = (float(*)[33])s_buf;
         prep_vec_tile<DK>(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
     }
+#ifdef TSDF_WG_TIMES
+    __syncthreads();
+    if (tid == 0 && rec) {
+        g_wg_times[1][b] = __builtin_amdgcn_s_memrealtime();
+        g_wg_times[2][b] = ((unsigned long long)(b < sg.gi ? 0 : b < sg.gi + sg.gc ? 1 : 2) << 32) |
+                           (b < sg.gi ? s_next : 0u);
+    }
+#endif
 }
 
 // Fold one launch's allocations (PoolState::cursor) into the free list / bump pointer (the
