@@ -125,6 +125,20 @@ def main():
         out.append(res)
         del ht
         torch.cuda.empty_cache()
+    # the reference's own table sizes (HashTable(map_size=1000000), hash_fusion.py:34; 2000000 in
+    # hash_demo1.py:110) against 2^22: the device table takes the next power of two of slots, so
+    # every size runs the fused launch; steady pass over the same frames after an allocating pass
+    sizes = {}
+    for ms in (1000000, 2000000, 1 << 22):
+        ht = table(0.02, ms, 1 << 15)
+        run(ht)  # allocate
+        best = min(run(ht)[0] for _ in range(3))
+        info = ht.info()
+        sizes[str(ms)] = {"frames_per_s": round(F / best, 1), "device_slots": int(info["slots"]),
+                          "table_size": int(ht._table_size), "blocks_live": int(info["used"])}
+        print(json.dumps({"reference_sizes": sizes}), file=sys.stderr, flush=True)
+        del ht
+        torch.cuda.empty_cache()
     # 1024^3 @ 1 cm extent (config[4]'s): the cull walks 2^21 bricks per batch
     ext = {}
     for vs, nb in ((0.02, 64 ** 3), (0.01, 128 ** 3)):
@@ -139,7 +153,7 @@ def main():
         print(json.dumps(ext), file=sys.stderr, flush=True)
         del ht
         torch.cuda.empty_cache()
-    print(json.dumps({"sweep": out, "frames": F, "slots": S, "extent_cost": ext,
+    print(json.dumps({"sweep": out, "frames": F, "slots": S, "extent_cost": ext, "reference_sizes": sizes,
                       "volume": "512^3 @ 2 cm extent, 8^3 blocks; steady pass = the first 64 bench-ring frames x 4",
                       "kernel": "k_fused_hash<0> (power-of-two device table, z-half waves)"}))
 

@@ -133,6 +133,7 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     if (dev < 0 || dev >= ndev) return set_error(TSDF_E_ARG, "device %d out of range [0,%d)", dev, ndev);
     device = dev;
     TSDF_HIP(hipSetDevice(device));
+    if (const char* e = getenv("TSDF_CULL_G")) cull_g = atoi(e);  // A/B override (Base::cull_per_wg)
     for (int a = 0; a < 3; ++a) {
         const int64_t o = off ? off[a] : 0;
         if (dims[a] <= 0 || o < 0 || dims[a] + o > (1 << 24))
@@ -195,6 +196,7 @@ int Base::sync_all() {
     if (cstream) TSDF_HIP(hipStreamSynchronize(cstream));
     return TSDF_OK;
 }
+
 
 int Base::ensure_pyr(int H, int W) {
     if (pyr_set[0] && H == pyr_H && W == pyr_W && pyr_set[n_sets - 1]) return TSDF_OK;

@@ -118,7 +118,7 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
     const int gi_occ = h->nz == 4 ? (int)B.grid_for((const void*)k_fused<true, 4>, kFusedWG)
                                   : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
     const int gi_full = h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ;
-    const int gc_full = (int)B.cull_grid();
+    const int gc_full = (int)B.cull_grid_fused();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;  // batch prepped by this launch
@@ -137,6 +137,7 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
         Stage sg{};
         sg.gi = has_i ? gi_full : 0;
         sg.gc = has_c ? gc_full : 0;
+        sg.cg = B.cull_per_wg();
         sg.ptx = (W + 63) / 64;
         sg.pty = (H + 63) / 64;
         if (has_i) {

@@ -1056,28 +1056,39 @@ __device__ inline void flush_stats(unsigned long long* s_stat, unsigned long lon
 // wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
 constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 8
 
-// Brick culling for one batch, hierarchical: one workgroup per superbrick (64 bricks, Vol::sb),
-// one wave per frame.  Wave f tests the superbrick against frame f (wave-uniform) and, if it
-// survives, each lane tests its brick against frame f; the per-brick frame masks meet in LDS and
-// wave 0 appends the kept bricks to the list (one atomicAdd per superbrick with survivors).
-// Every test is at most two cull_brick latencies deep, whatever the batch size.
+// Brick culling for one batch, hierarchical: one workgroup per G superbricks (64 bricks each,
+// Vol::sb), one wave per (superbrick, frame) pair at a time.  The wave tests the superbrick against
+// the frame (wave-uniform) and, if it survives, each lane tests its brick against the frame; the
+// per-brick frame masks meet in LDS and wave g appends superbrick g's kept bricks to the list (one
+// atomicAdd per cost class with survivors).  Every test is at most two cull_brick latencies deep;
+// a wave takes ceil(G * frames / waves) pairs in turn.  G > 1 (fused launches over large volumes,
+// Base::cull_per_wg): the test is latency-bound, so a workgroup's fixed costs (start, barriers,
+// list atomics, statistics) are shared by G superbricks and the stage takes fewer of the CUs'
+// slots while the integrate still runs (+1.8 % at 512^3); on small shards the cull runs in the
+// launch's tail, where its latency counts, and G = 1.
+constexpr int kCullGMax = 4;
 template <bool HASH, bool P2 = false>
 __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Table& tab, ListEntry* list,
-                                       unsigned int* count, unsigned long long* stats, int si,
-                                       unsigned* s_mask, unsigned long long* s_stat, int* res = nullptr) {
+                                       unsigned int* count, unsigned long long* stats, int wgi,
+                                       unsigned* s_mask, unsigned long long* s_stat, int* res = nullptr,
+                                       int G = 1) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int f0 = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (tid < 64) s_mask[tid] = 0u;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), n_waves = (int)(blockDim.x >> 6);
+    if (tid < 64 * G) s_mask[tid] = 0u;
     if (tid < kNStat) s_stat[tid] = 0;
     __syncthreads();
+    const int nsx = (v.nb[0] + (1 << v.sb[0]) - 1) >> v.sb[0];
     const int nsy = (v.nb[1] + (1 << v.sb[1]) - 1) >> v.sb[1];
     const int nsz = (v.nb[2] + (1 << v.sb[2]) - 1) >> v.sb[2];
-    const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
+    const int n_sb = nsx * nsy * nsz;
     const int ex = 1 << v.sb[0], ey = 1 << v.sb[1], ez = 1 << v.sb[2];
     const int lz = lane & (ez - 1), ly = (lane >> v.sb[2]) & (ey - 1), lx = lane >> (v.sb[1] + v.sb[2]);
-    const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
-    const unsigned e = (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz);
-    for (int f = f0; f < bt.n; f += kCullWG / 64) {  // wave w: frames w, w + 8
+    for (int p = wave; p < G * bt.n; p += n_waves) {  // (superbrick g, frame f) pairs
+        const int g = p / bt.n, f = p - g * bt.n;
+        const int si = wgi * G + g;
+        if (si >= n_sb) continue;
+        const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
+        const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
         const Frame& fr = bt.f[f];
         if (cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
             bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
@@ -1085,12 +1096,16 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
                 const long long home = ref_hash<P2>(bx, by, bz, tab.shard_cap, tab.int_bits);
                 test = shard_of<P2>(home, v.n_shards, tab.shard_cap) == v.shard;
             }
-            if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
+            if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[g * 64 + lane], 1u << f);
         }
     }
     __syncthreads();
-    if (tid < 64) {  // append the kept bricks to the sub-list of their cost class (frames kept)
-        const unsigned fmask = s_mask[lane];
+    const int si = wgi * G + wave;
+    if (wave < G && si < n_sb) {  // append the kept bricks to the sub-list of their cost class (frames kept)
+        const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
+        const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
+        const unsigned e = (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz);
+        const unsigned fmask = s_mask[wave * 64 + lane];
         const int cls = __popc(fmask);
         const unsigned long long any = __ballot(cls != 0);
         if (any) {
@@ -1103,7 +1118,7 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
             }
             unsigned base = 0;  // lanes 1..8 reserve their class's slots at once
             if (lane >= 1 && lane <= kMaxBatch && n_cls) base = atomicAdd(&count[lane], n_cls);
-            if (lane == 0) s_stat[ST_VISITED] = (unsigned long long)__popcll(any);
+            if (lane == 0) atomicAdd(&s_stat[ST_VISITED], (unsigned long long)__popcll(any));
             base = __shfl(base, cls);
             const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
             if (cls && base + rank < nbk) {
@@ -1437,6 +1452,7 @@ struct Stage {
     unsigned int* count_c;
     unsigned int* count_p;   // prep: count of batch k+2 (reset for its cull)
     int gi, gc;              // integrate / cull workgroups
+    int cg;                  // superbricks per cull workgroup (<= kCullGMax)
     int ptx, pty;            // prep tiles per frame (x, y)
     long long seq;           // hash: launch number for the pool report (Table::rb)
     int* res_i;              // hash: per-brick claim words of batch k (integrate) and k+1 (cull)
@@ -1479,7 +1495,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
         cull_superbrick<false>(v, bc, no_table, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
-                               s_stat);
+                               s_stat, nullptr, sg.cg);
     } else {
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;
@@ -1554,7 +1570,7 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         }
     } else if (b < sg.gi + sg.gc) {
         cull_superbrick<true, true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
-                                    s_stat, sg.res_c);
+                                    s_stat, sg.res_c, sg.cg);
     } else {
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;

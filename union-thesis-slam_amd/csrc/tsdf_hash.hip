@@ -858,7 +858,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         TSDF_HIP(hipMalloc(&h->d_res, sizeof(int) * kSets * (size_t)B.n_bricks));
     }
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
-    const int gc_full = (int)B.cull_grid();
+    const int gc_full = (int)B.cull_grid_fused();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;
@@ -878,6 +878,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         Stage sg{};
         sg.gi = has_i ? gi_full : 0;
         sg.gc = has_c ? gc_full : 0;
+        sg.cg = B.cull_per_wg();
         sg.ptx = (W + 63) / 64;
         sg.pty = (H + 63) / 64;
         if (has_i) {

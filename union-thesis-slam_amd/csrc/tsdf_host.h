@@ -161,6 +161,16 @@ struct Base {
         for (int a = 0; a < 3; ++a) n *= (vol.nb[a] + (1 << vol.sb[a]) - 1) >> vol.sb[a];
         return (unsigned)n;
     }
+    // Superbricks per cull workgroup of a fused launch: 3 where the volume has >= 1024 superbricks
+    // (the cull runs beside the integrate's tail: fewer slots taken, measured +2 % at 1, 2 and 4
+    // ranks), 1 on smaller shards (the cull IS the launch's tail there: 3 cost 4.6 % on an eighth
+    // shard); TSDF_CULL_G overrides.  And the cull workgroups of such a launch.
+    int cull_g = 0;  // (0: by the rule)
+    int cull_per_wg() const {
+        if (cull_g > 0) return cull_g < kCullGMax ? cull_g : kCullGMax;
+        return cull_grid() >= 1024 ? 3 : 1;
+    }
+    unsigned cull_grid_fused() const { return (cull_grid() + cull_per_wg() - 1) / cull_per_wg(); }
     int read_stats(tsdf_stats_t* out, int reset);
     // Vol::canon from the first n_vox voxels of the pool (after a set or an import; synchronous)
     int check_canon(long long n_vox);
