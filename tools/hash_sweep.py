@@ -131,7 +131,7 @@ def main():
     sizes = {}
     for ms in (1000000, 2000000, 1 << 22):
         ht = table(0.02, ms, 1 << 15)
-        run(ht)  # allocate
+        run(ht, sync=True)  # allocate (a fresh pool's growth, overflow re-runs exact)
         best = min(run(ht)[0] for _ in range(3))
         info = ht.info()
         sizes[str(ms)] = {"frames_per_s": round(F / best, 1), "device_slots": int(info["slots"]),

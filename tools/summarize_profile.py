@@ -29,7 +29,7 @@ def per_kernel(path, counter):
     return out
 
 
-def main(tag="r02"):
+def main(tag):
     src = os.path.join(REPO, "gpurun_out", "profile")
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
