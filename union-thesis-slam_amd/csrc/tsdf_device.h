@@ -158,6 +158,8 @@ struct Table {
     long long capacity;
     long long shard_cap;        // capacity at create: bucket-range ownership stays fixed across resizes
     long long max_blocks;
+    const int* owned;           // bucket-range shards: the bricks this shard owns, increasing (else null)
+    int n_owned;
     int overflow_cap;
     int int_bits;               // 64: NumPy int64; 32: wrapping int32 (author's Windows run)
 };
@@ -1056,6 +1058,33 @@ __device__ inline void flush_stats(unsigned long long* s_stat, unsigned long lon
 // wave ballot + LDS prefix over the 4 waves + ONE atomicAdd per workgroup.
 constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 8
 
+// Wave-level append of the kept bricks (lane: brick e, its frame mask) to the sub-list of their cost
+// class (frames kept): one atomicAdd per class with survivors.
+template <bool HASH>
+__device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* count, unsigned long long* s_stat,
+                                   int* res, unsigned e, unsigned fmask) {
+    const int lane = lane_id();
+    const int cls = __popc(fmask);
+    const unsigned long long any = __ballot(cls != 0);
+    if (!any) return;
+    unsigned n_cls = 0, rank = 0;
+#pragma unroll
+    for (int c = 1; c <= kMaxBatch; ++c) {
+        const unsigned long long m = __ballot(cls == c);
+        if (lane == c) n_cls = (unsigned)__popcll(m);
+        if (cls == c) rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    unsigned base = 0;  // lanes 1..8 reserve their class's slots at once
+    if (lane >= 1 && lane <= kMaxBatch && n_cls) base = atomicAdd(&count[lane], n_cls);
+    if (lane == 0) atomicAdd(&s_stat[ST_VISITED], (unsigned long long)__popcll(any));
+    base = __shfl(base, cls);
+    const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
+    if (cls && base + rank < nbk) {
+        list[(size_t)(cls - 1) * nbk + base + rank] = (ListEntry)e | ((ListEntry)fmask << 32);
+        if (HASH && res) res[e] = kResFree;  // the brick's claim word for this batch
+    }
+}
+
 // Brick culling for one batch, hierarchical: one workgroup per G superbricks (64 bricks each,
 // Vol::sb), one wave per (superbrick, frame) pair at a time.  The wave tests the superbrick against
 // the frame (wave-uniform) and, if it survives, each lane tests its brick against the frame; the
@@ -1104,29 +1133,37 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
     if (wave < G && si < n_sb) {  // append the kept bricks to the sub-list of their cost class (frames kept)
         const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
         const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
-        const unsigned e = (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz);
-        const unsigned fmask = s_mask[wave * 64 + lane];
-        const int cls = __popc(fmask);
-        const unsigned long long any = __ballot(cls != 0);
-        if (any) {
-            unsigned n_cls = 0, rank = 0;
-#pragma unroll
-            for (int c = 1; c <= kMaxBatch; ++c) {
-                const unsigned long long m = __ballot(cls == c);
-                if (lane == c) n_cls = (unsigned)__popcll(m);
-                if (cls == c) rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-            }
-            unsigned base = 0;  // lanes 1..8 reserve their class's slots at once
-            if (lane >= 1 && lane <= kMaxBatch && n_cls) base = atomicAdd(&count[lane], n_cls);
-            if (lane == 0) atomicAdd(&s_stat[ST_VISITED], (unsigned long long)__popcll(any));
-            base = __shfl(base, cls);
-            const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
-            if (cls && base + rank < nbk) {
-                list[(size_t)(cls - 1) * nbk + base + rank] = (ListEntry)e | ((ListEntry)fmask << 32);
-                if (HASH && res) res[e] = kResFree;  // the brick's claim word for this batch
-            }
-        }
+        append_kept<HASH>(v, list, count, s_stat, res, (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz),
+                          s_mask[wave * 64 + lane]);
     }
+    __syncthreads();
+    flush_stats(s_stat, stats);
+}
+
+// The cull of a bucket-range hash shard (Table::owned): its bricks are spread over the whole
+// extent (one in n_shards, by home bucket), so instead of walking every superbrick of the extent it
+// walks only the bricks the shard owns, 64 per workgroup (lane = brick, one wave per frame at a
+// time: one brick test deep, no superbrick level).  An eighth shard culls an eighth of the bricks.
+template <bool HASH>
+__device__ inline void cull_owned(const Vol& v, const Batch& bt, const Table& tab, ListEntry* list,
+                                  unsigned int* count, unsigned long long* stats, int wgi, unsigned* s_mask,
+                                  unsigned long long* s_stat, int* res) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), n_waves = (int)(blockDim.x >> 6);
+    if (tid < 64) s_mask[tid] = 0u;
+    if (tid < kNStat) s_stat[tid] = 0;
+    __syncthreads();
+    const int i = wgi * 64 + lane;
+    const bool have = i < tab.n_owned;
+    const int e = have ? tab.owned[i] : 0;
+    const int nb12 = v.nb[1] * v.nb[2];
+    const int bx = e / nb12, r = e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
+    for (int f = wave; f < bt.n; f += n_waves) {
+        const Frame& fr = bt.f[f];
+        if (have && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
+    }
+    __syncthreads();
+    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
@@ -1136,7 +1173,8 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, Li
                                                   unsigned int* count, unsigned long long* stats) {
     __shared__ unsigned s_mask[64];
     __shared__ unsigned long long s_stat[kNStat];
-    cull_superbrick<HASH>(v, bt, tab, list, count, stats, blockIdx.x, s_mask, s_stat);
+    if (HASH && tab.owned) cull_owned<HASH>(v, bt, tab, list, count, stats, blockIdx.x, s_mask, s_stat, nullptr);
+    else cull_superbrick<HASH>(v, bt, tab, list, count, stats, blockIdx.x, s_mask, s_stat);
 }
 
 // Integrate the listed bricks: each wave takes list entries gw, gw + NW, ... (NW = waves in the
@@ -1569,8 +1607,11 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
             commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq);
         }
     } else if (b < sg.gi + sg.gc) {
-        cull_superbrick<true, true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
-                                    s_stat, sg.res_c, sg.cg);
+        if (tab.owned)
+            cull_owned<true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf, s_stat, sg.res_c);
+        else
+            cull_superbrick<true, true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
+                                        s_stat, sg.res_c, sg.cg);
     } else {
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;

@@ -858,7 +858,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         TSDF_HIP(hipMalloc(&h->d_res, sizeof(int) * kSets * (size_t)B.n_bricks));
     }
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
-    const int gc_full = (int)B.cull_grid_fused();
+    const int gc_full = h->t.owned ? (h->t.n_owned + 63) / 64 : (int)B.cull_grid_fused();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;
@@ -933,7 +933,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
              int H, int W, const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     TSDF_HIP(hipSetDevice(B.device));
-    const unsigned cull_grid = B.cull_grid();
+    const unsigned cull_grid = h->t.owned ? (unsigned)std::max(1, (h->t.n_owned + 63) / 64) : B.cull_grid();
     const bool sync = !(flags & TSDF_ASYNC);
     if (!sync && h->rb_used < 0 && n_frames > kMaxBatch && B.prestaged < 0) {
         // A fresh table's first asynchronous call: its first batch runs synchronously (the pool
@@ -1114,6 +1114,22 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
         if (e == hipSuccess) e = hipMalloc(&t.vals, sizeof(int) * t.capacity);
         if (e == hipSuccess) e = hipMalloc(&t.overflow, sizeof(ListEntry) * (size_t)t.overflow_cap);
         if (e == hipSuccess) e = hipMalloc(&t.st, sizeof(PoolState));
+        if (e == hipSuccess && n_shards > 1) {
+            // the bricks this bucket-range shard owns (fixed at create, Table::shard_cap), for the
+            // cull (cull_owned): increasing brick index
+            const Vol& v = h->b.vol;
+            std::vector<int> own;
+            own.reserve((size_t)(h->b.n_bricks / n_shards + 64));
+            for (int bx = 0; bx < v.nb[0]; ++bx)
+                for (int by = 0; by < v.nb[1]; ++by)
+                    for (int bz = 0; bz < v.nb[2]; ++bz)
+                        if (shard_of(ref_hash(bx, by, bz, t.shard_cap, int_bits), n_shards, t.shard_cap) == shard)
+                            own.push_back((bx * v.nb[1] + by) * v.nb[2] + bz);
+            t.n_owned = (int)own.size();
+            e = hipMalloc((void**)&t.owned, sizeof(int) * std::max<size_t>(own.size(), 1));
+            if (e == hipSuccess && !own.empty())
+                e = hipMemcpy((void*)t.owned, own.data(), sizeof(int) * own.size(), hipMemcpyHostToDevice);
+        }
         // the pool: address ranges for every brick of the volume, backed as it grows
         // (TSDF_HASH_VMM=0: plain allocations, grown by copy)
         const char* ev = getenv("TSDF_HASH_VMM");
@@ -1173,7 +1189,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
     if (!h) return TSDF_OK;
     (void)hipSetDevice(h->b.device);
     h->b.release();
-    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res};
+    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res, (void*)h->t.owned};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (h->vmm) {
