@@ -1085,12 +1085,13 @@ __device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* 
     }
 }
 
-// Brick culling for one batch, hierarchical: one workgroup per G superbricks (64 bricks each,
-// Vol::sb), one wave per (superbrick, frame) pair at a time.  The wave tests the superbrick against
-// the frame (wave-uniform) and, if it survives, each lane tests its brick against the frame; the
+// Brick culling for one batch: one workgroup per G superbricks (64 bricks each, Vol::sb), one wave
+// per (superbrick, frame) pair at a time, each lane testing its brick against the frame; the
 // per-brick frame masks meet in LDS and wave g appends superbrick g's kept bricks to the list (one
-// atomicAdd per cost class with survivors).  Every test is at most two cull_brick latencies deep;
-// a wave takes ceil(G * frames / waves) pairs in turn.  G > 1 (fused launches over large volumes,
+// atomicAdd per cost class with survivors).  A test is one cull_brick deep; a wave takes
+// ceil(G * frames / waves) pairs in turn.  (Round 3 dropped the superbrick-level test that ran
+// first: an invisible brick leaves cull_brick at its bounding-sphere test anyway, and a visible
+// superbrick cost two test latencies instead of one -- +2.7 % dense, +2.6 % on an eighth shard.)  G > 1 (fused launches over large volumes,
 // Base::cull_per_wg): the test is latency-bound, so a workgroup's fixed costs (start, barriers,
 // list atomics, statistics) are shared by G superbricks and the stage takes fewer of the CUs'
 // slots while the integrate still runs (+1.8 % at 512^3); on small shards the cull runs in the
@@ -1119,14 +1120,12 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
         const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
         const Frame& fr = bt.f[f];
-        if (cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, sx * ex, sy * ey, sz * ez, ex, ey, ez))) {
-            bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
-            if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership
-                const long long home = ref_hash<P2>(bx, by, bz, tab.shard_cap, tab.int_bits);
-                test = shard_of<P2>(home, v.n_shards, tab.shard_cap) == v.shard;
-            }
-            if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[g * 64 + lane], 1u << f);
+        bool test = bx < v.nb[0] && by < v.nb[1] && bz < v.nb[2];
+        if (HASH && v.n_shards > 1 && test) {  // bucket-range ownership (shards use cull_owned)
+            const long long home = ref_hash<P2>(bx, by, bz, tab.shard_cap, tab.int_bits);
+            test = shard_of<P2>(home, v.n_shards, tab.shard_cap) == v.shard;
         }
+        if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[g * 64 + lane], 1u << f);
     }
     __syncthreads();
     const int si = wgi * G + wave;
