@@ -45,10 +45,11 @@ VOXEL = 0.02
 PIX = 640 * 480
 BATCH = 8  # frames per step (kMaxBatch)
 WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) into 512^3 @ 2 cm dense grid"
-# the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), used when their
-# workload matches: DRAM-side traffic (FETCH_SIZE / WRITE_SIZE) and VALU issue (SQ counters)
-PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r03.json")
-SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r03.json")
+# the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), quoted only when
+# their workload AND the build id of the library they measured match the loaded library
+# (tsdf_build_id): DRAM-side traffic (FETCH_SIZE / WRITE_SIZE) and VALU issue (SQ counters)
+PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r04.json")
+SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r04.json")
 
 
 def log(*a):
@@ -75,7 +76,77 @@ def parse():
                     help="A/B: keep the resident depth as float64 metres (the f64-texel integrate)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: several ranks may share a GPU)")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)  # tests: ranks, no GPU
     return ap.parse_args()
+
+
+def self_launch(args):
+    """`--gpus N` (N > 1) run without a launcher: start N ranks of this script under
+    torch.distributed.run as a CHILD process (nothing here has touched a GPU), relay its output
+    and return its exit code -- never a silent one-rank line."""
+    import socket
+    import subprocess
+    if args.dist_backend == "nccl":
+        import torch
+        have = torch.cuda.device_count()  # (does not initialise the GPU on this image)
+        if have < args.gpus:
+            log(f"error: --gpus {args.gpus} with RCCL needs {args.gpus} GPUs, {have} visible "
+                "(--dist-backend gloo rehearses several ranks on fewer GPUs)")
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching " + " ".join(cmd[1:]))
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    return subprocess.call(cmd, env=env)
+
+
+def attach_profiles(roof, st, build_id):
+    """Attach the committed PMC traffic / SQ issue profiles to the roofline block, only when they
+    measured this workload with this exact library build; otherwise say why they are absent."""
+    why = []
+    for path, key in ((PMC_PROFILE, "traffic"), (SQ_PROFILE, "valu")):
+        rel = os.path.relpath(path, REPO)
+        if not os.path.exists(path):
+            why.append(f"{key}: no {rel}")
+            continue
+        with open(path) as fh:
+            p = json.load(fh)
+        if p.get("workload") != WORKLOAD:
+            why.append(f"{key}: {rel} measured another workload")
+            continue
+        if p.get("build_id") != build_id:
+            why.append(f"{key}: {rel} measured library build {p.get('build_id')}, this is {build_id}")
+            continue
+        avg_s = roof["kernel_avg_us"] / 1e6
+        if key == "traffic" and p.get("hbm_bytes_per_launch"):
+            tb = float(p["hbm_bytes_per_launch"])
+            roof["traffic"] = round(tb)
+            # measured DRAM-side bytes over this run's average launch time
+            roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            roof["traffic_source"] = (rel + " (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH "
+                                      "doubled per the gfx950 rule; build " + build_id + ")")
+        med = p.get("median_per_launch", {})
+        if key == "valu" and med.get("SQ_INSTS_VALU"):
+            vox_launch = st["voxel_updates"] / st["kernel_launches"]
+            roof["valu"] = {
+                "valu_busy": p["valu_busy_per_simd"],
+                "valu_wave_insts_per_launch": round(med["SQ_INSTS_VALU"]),
+                "valu_lane_insts_per_voxel_update": round(64.0 * med["SQ_INSTS_VALU"] / vox_launch, 1),
+                "source": rel + " (rocprofv3 --pmc SQ pass of the same kernel, workload and build; busy = "
+                          "SQ_ACTIVE_INST_VALU x 4 / SIMD cycles)"}
+            # the binding resource: the one closer to its peak (VALU issue vs measured DRAM bytes;
+            # the algorithmic bytes count every update's state traffic, which temporal batching
+            # keeps on chip)
+            if roof.get("traffic_frac") is not None and p["valu_busy_per_simd"] > roof["traffic_frac"]:
+                roof["bound"] = "valu"
+                roof["bound_note"] = ("VALU issue-bound: the SIMDs issue VALU in valu_busy of their cycles "
+                                      "while DRAM moves traffic_frac of its peak; achieved/peak/frac are the "
+                                      "algorithmic-bytes HBM roofline of the contract")
+    if why:
+        roof["profiles_note"] = "; ".join(why)
 
 
 def frame_ranges(start, count, F):
@@ -184,12 +255,23 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.gpus != world:
+        log(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE {world} ranks")
+        sys.exit(2)
     n = world
+    if args.launch_selftest:  # the launch path alone (CPU tests): ranks meet over gloo, no GPU
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"selftest": True, "n_gpus": n, "ranks_seen": int(t.item())}), flush=True)
+        dist.destroy_process_group()
+        return
     gpu = local if args.dist_backend == "nccl" else local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -279,36 +361,7 @@ def main():
                 "kernel_avg_us": round(1e6 * avg_s, 2),
                 "bytes_per_launch": round(alg_bytes / st["kernel_launches"]),
                 "launches": st["kernel_launches"]}
-        if os.path.exists(PMC_PROFILE):
-            with open(PMC_PROFILE) as fh:
-                p = json.load(fh)
-            if p.get("workload") == WORKLOAD and p.get("hbm_bytes_per_launch"):
-                tb = float(p["hbm_bytes_per_launch"])
-                roof["traffic"] = round(tb)
-                # measured DRAM-side bytes over this run's average launch time
-                roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
-                roof["traffic_source"] = (os.path.relpath(PMC_PROFILE, REPO) + " (separate rocprofv3 --pmc "
-                                          "FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 rule)")
-        if os.path.exists(SQ_PROFILE):
-            with open(SQ_PROFILE) as fh:
-                q = json.load(fh)
-            med = q.get("median_per_launch", {})
-            if q.get("workload") == WORKLOAD and med.get("SQ_INSTS_VALU"):
-                vox_launch = st["voxel_updates"] / st["kernel_launches"]
-                roof["valu"] = {
-                    "valu_busy": q["valu_busy_per_simd"],
-                    "valu_wave_insts_per_launch": round(med["SQ_INSTS_VALU"]),
-                    "valu_lane_insts_per_voxel_update": round(64.0 * med["SQ_INSTS_VALU"] / vox_launch, 1),
-                    "source": os.path.relpath(SQ_PROFILE, REPO) + " (rocprofv3 --pmc SQ pass of the same "
-                              "kernel and workload; busy = SQ_ACTIVE_INST_VALU x 4 / SIMD cycles)"}
-                # the binding resource: the one closer to its peak (VALU issue vs measured DRAM bytes;
-                # the algorithmic bytes above count every update's state traffic, which temporal
-                # batching keeps on chip)
-                if roof.get("traffic_frac") is not None and q["valu_busy_per_simd"] > roof["traffic_frac"]:
-                    roof["bound"] = "valu"
-                    roof["bound_note"] = ("VALU issue-bound: the SIMDs issue VALU in valu_busy of their cycles "
-                                          "while DRAM moves traffic_frac of its peak; achieved/peak/frac are the "
-                                          "algorithmic-bytes HBM roofline of the contract")
+        attach_profiles(roof, st, _ffi.build_id())
     vf_mean = st["voxel_updates"] / Kf
     log(f"[rank {rank}] dense: {Kf} frames in {dt * 1e3:.1f} ms -> {Kf / dt:.0f} frames/s, "
         f"V_f mean {vf_mean:.0f} ({100 * vf_mean / (len(vol.x_index) * X * X):.1f}% of shard), "
@@ -541,6 +594,7 @@ def main():
             "value": round(fps, 1), "unit": "frames/s", "n_gpus": n, "steps": Ks, "warmup": W,
             "ms_per_step": round(1e3 * dt_max / Ks, 4), "frames_per_step": BATCH,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "build_id": _ffi.build_id(),
             "data": "synthetic (ray-cast 10.24 m room + spheres, u16 mm depth, RGB8; generated in HBM)",
             "config": {"workload": WORKLOAD, "volume": "512x512x512 @ 0.02 m", "frames_resident": F,
                        "image": "640x480", "timed_frames": Kf,

@@ -92,6 +92,10 @@ typedef struct {
 } tsdf_hash_info_t;
 
 const char* tsdf_last_error(void);
+/* Build id of the loaded library: the first 16 hex digits of the sha256 of the sources it was
+ * compiled from (csrc/, this header, the Makefile).  Profiles under profiles/ record the id of
+ * the library they measured; bench.py quotes a profile's counters only for the same id. */
+const char* tsdf_build_id(void);
 int tsdf_device_count(int* n);
 
 /* ---- dense grid: replaces TSDFVolume (grid_fusion.py:19-320) ------------------------------

@@ -27,7 +27,20 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     # every declared entry point is typed by the binding
-    assert set(names) - {"tsdf_last_error"} == set(_ffi.SIGNATURES)
+    assert set(names) - {"tsdf_last_error", "tsdf_build_id"} == set(_ffi.SIGNATURES)
+
+
+def test_build_id_names_the_sources():
+    """tsdf_build_id() is the sha256 prefix of the sources the library was built from (the
+    Makefile's BUILD_ID), so profiles can be matched to the library they measured."""
+    import subprocess
+    from tsdf_amd import _ffi
+    bid = _ffi.build_id()
+    assert len(bid) == 16 and int(bid, 16) >= 0
+    pkg = os.path.join(REPO, "union-thesis-slam_amd")
+    want = subprocess.run(["make", "-s", "-C", pkg, "--eval", "print-id: ; @echo $(BUILD_ID)", "print-id"],
+                          capture_output=True, text=True, check=True).stdout.strip()
+    assert bid == want, "the built library is stale: rebuild with make -C union-thesis-slam_amd"
 
 
 def test_library_is_gfx950_code_object():

@@ -261,3 +261,49 @@ def test_trim_hands_pool_memory_back_and_growth_resumes(monkeypatch):
     for a, b in zip(g.get_state(), h.get_state()):
         assert np.array_equal(a, b)
     assert h.stats()["bricks_skipped"] == 0 or h.info()["pool_capacity"] > after["pool_capacity"]
+
+
+def test_async_hash_growth_survives_a_turn_into_unseen_space():
+    """Advisor r03: asynchronous pool growth must not lag a growth spike.  A long steady stretch
+    (the same eight frames re-integrated: no new blocks, so the recent growth is ~0), then the
+    camera jumps to a far part of the trajectory (thousands of new blocks per batch): the room kept
+    for the launches in flight covers two batches' cull lists, so nothing is skipped and no
+    TSDF_E_CAPACITY is raised; the result equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    d0, c0, p0 = _synth(8, start=100)
+    d1, c1, p1 = _synth(24, start=560)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    d = np.concatenate([d0] * 5 + [d1])
+    c = np.concatenate([c0] * 5 + [c1])
+    Tinv = np.linalg.inv(np.concatenate([p0] * 5 + [p1]))
+    h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 16, max_blocks=1 << 12)
+    h.integrate_batch(d[:8], c[:8], K, Tinv[:8])  # synchronous start
+    h.integrate_batch(d[8:], c[8:], K, Tinv[8:], sync=False)
+    h.sync()  # raises TSDF_E_CAPACITY if a launch in flight ran out of pool
+    assert h.stats()["bricks_skipped"] == 0
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
+    g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+
+
+def test_trim_integrate_trim_integrate_stays_exact():
+    """Advisor r03: every trim compacts the pool into fresh address ranges and retires the old ones
+    (kept reserved until the handle is destroyed, never handed out again); trim / integrate cycles
+    keep the state bit-identical to the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    d, c, poses = _synth(48, start=200)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 16, max_blocks=1 << 12)
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
+    h.integrate_batch(d[:8], c[:8], K, Tinv[:8])
+    for k in range(1, 6):
+        lo, hi = 8 * k, 8 * (k + 1)
+        h.integrate_batch(d[lo:hi], c[lo:hi], K, Tinv[lo:hi], sync=(k % 2 == 0))
+        h.trim()
+        h.trim()  # a second trim in a row: nothing to gain, nothing changes
+    g.integrate_batch(d, c, K, Tinv)
+    assert h.info()["pool_mapped"] == 1
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)

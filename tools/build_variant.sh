@@ -7,7 +7,7 @@ W=$(mktemp -d /tmp/abvar.XXXX)
 mkdir -p "$W/pkg" "$W/include"
 cp -r "$R/union-thesis-slam_amd/csrc" "$R/union-thesis-slam_amd/Makefile" "$W/pkg/"
 cp "$R/include/"*.h "$W/include/"
-make -s -C "$W/pkg" HIPFLAGS="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -Wno-bitwise-instead-of-logical -I../include -Icsrc $2" >/dev/null
+make -s -C "$W/pkg" EXTRA="$2" >/dev/null
 mkdir -p "$R/abtest"
 cp "$W/pkg/tsdf_amd/lib/libtsdf_hip.so" "$R/abtest/lib$1.so"
 rm -rf "$W"

@@ -144,7 +144,8 @@ struct PoolState {
 constexpr int kReports = 8;
 struct PoolReport {
     long long pool_top, free_count, n_overflow;
-    long long seq;  // launch number + 1 (0: slot never written)
+    long long listed;  // bricks the launch's cull listed: a bound on the blocks one batch can allocate
+    long long seq;     // launch number + 1 (0: slot never written)
 };
 
 struct Table {
@@ -1552,7 +1553,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
 // Fold one launch's allocations (PoolState::cursor) into the free list / bump pointer (the
 // hash's k_commit, also run by the last integrate workgroup of a fused hash launch).
 __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolReport* rb = nullptr,
-                                   long long seq = -1) {
+                                   long long seq = -1, const unsigned* count = nullptr) {
     const long long used = coh_load(&st->cursor);
     const long long nf = coh_load(&st->free_count);
     const long long cons = used < nf ? used : nf;
@@ -1566,6 +1567,10 @@ __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolRepo
         __hip_atomic_store(&r->pool_top, top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&r->free_count, nf - cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&r->n_overflow, coh_load(&st->n_overflow), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        long long listed = 0;  // the batch's cost-class sub-list lengths (the integrate's list)
+        if (count)
+            for (int c = 1; c <= kMaxBatch; ++c) listed += coh_load(&((unsigned*)count)[c]);
+        __hip_atomic_store(&r->listed, listed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&r->seq, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -1603,7 +1608,7 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         __syncthreads();
         if (s_last && tid == 0) {
             __threadfence();
-            commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq);
+            commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq, sg.count_i);
         }
     } else if (b < sg.gi + sg.gc) {
         if (tab.owned)

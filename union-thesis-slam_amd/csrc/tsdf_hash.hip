@@ -105,7 +105,12 @@ struct VArray {
             (void)hipMemRelease(c.first);
         }
     }
-    void release() {
+    // Unmap and release the physical memory.  The address range itself goes into `retired` when
+    // kernels may have used it (kept reserved until the handle is destroyed, so no later reservation
+    // -- a trim's or a growth's -- can be handed the same virtual addresses and map over a range
+    // whose stale translations lost writes before, see above); with retired == nullptr (a range
+    // no kernel has touched, or the handle's end) it is freed at once.
+    void release(std::vector<std::pair<char*, size_t>>* retired = nullptr) {
         size_t off = mapped;
         for (auto it = chunks.rbegin(); it != chunks.rend(); ++it) {
             off -= it->second;
@@ -113,7 +118,10 @@ struct VArray {
             (void)hipMemRelease(it->first);
         }
         chunks.clear();
-        if (base) (void)hipMemAddressFree(base, reserved);
+        if (base) {
+            if (retired) retired->emplace_back(base, reserved);
+            else (void)hipMemAddressFree(base, reserved);
+        }
         base = nullptr;
         mapped = reserved = 0;
     }
@@ -167,6 +175,9 @@ struct tsdf_hash {
     // block pool on reserved address ranges (tsdf, weight, colour, entry words, free list)
     bool vmm = false;
     VArray va[5];
+    // address ranges of pool arrays that kernels used and that were since compacted away (trim) or
+    // replaced by plain allocations: unmapped, but reserved until destroy (VArray::release)
+    std::vector<std::pair<char*, size_t>> retired_va;
     int vmm_fail_at = -1;  // test hook (TSDF_HASH_VMM_FAIL=k): the next growth of array k fails
     static constexpr size_t kPer[5] = {sizeof(float) * kBrickVox, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
                                        sizeof(unsigned long long) * 8, sizeof(int)};
@@ -222,8 +233,9 @@ __global__ void k_fill_keys(unsigned long long* k, long long n) {
 }
 
 // After each allocating launch: fold the launch's allocations into the pool state.
-__global__ void k_commit(PoolState* st, long long max_blocks, PoolReport* rb, long long seq) {
-    commit_pool(st, max_blocks, rb, seq);
+__global__ void k_commit(PoolState* st, long long max_blocks, PoolReport* rb, long long seq,
+                         const unsigned* count) {
+    commit_pool(st, max_blocks, rb, seq, count);
 }
 
 // Single-thread linear probe; returns the slot or -1.
@@ -595,7 +607,7 @@ int grow_pool(tsdf_hash* h, long long new_max) {
     TSDF_HIP(hipStreamSynchronize(B.stream));
     fresh.keep();
     if (h->vmm) {
-        for (auto& v : h->va) v.release();
+        for (auto& v : h->va) v.release(&h->retired_va);
         h->vmm = false;
     } else {
         (void)hipFree(B.pool.tsdf);
@@ -638,13 +650,13 @@ int trim_pool(tsdf_hash* h) {
                                 h->b.stream) == hipSuccess;
         ok = ok && hipStreamSynchronize(h->b.stream) == hipSuccess;
     }
-    if (!ok) {  // keep the pool as it is
+    if (!ok) {  // keep the pool as it is (copies may have written the new ranges: retire them too)
         (void)hipGetLastError();
-        for (auto& v : nv) v.release();
+        for (auto& v : nv) v.release(&h->retired_va);
         return TSDF_OK;
     }
     for (int k = 0; k < 5; ++k) {
-        h->va[k].release();
+        h->va[k].release(&h->retired_va);
         h->va[k] = nv[k];
         nv[k] = VArray{};
     }
@@ -761,12 +773,17 @@ int wait_report(tsdf_hash* h, long long s, PoolReport* out) {
     out->pool_top = r->pool_top;
     out->free_count = r->free_count;
     out->n_overflow = r->n_overflow;
+    out->listed = r->listed;
     out->seq = s + 1;
     return TSDF_OK;
 }
 
 // Asynchronous calls, before issuing allocating launch s: launches s-1 and s may allocate before
-// the next check, so keep room for three times the largest growth seen between two launches.
+// the next check.  Each can allocate at most the bricks its cull lists, and a batch's list is
+// about as long as the one before it (the camera moves a little per batch), so the room kept is
+// two of launch s-2's lists -- a bound that holds when the camera turns from a region it has
+// mapped to one it has not (growth jumps from ~0 to the whole list), where the recent growth
+// alone would not -- or three recent growths when larger.
 int async_room(tsdf_hash* h, long long s) {
     if (s < 2) return TSDF_OK;
     PoolReport r;
@@ -774,10 +791,9 @@ int async_room(tsdf_hash* h, long long s) {
     if (r.n_overflow > 0) return take_overflow(h);
     const long long used = r.pool_top - r.free_count;
     h->note_live(used);
-    // launches s-1 and s may allocate before the next check: room for three recent growths (the
-    // copy path keeps the pool's 1/12 as a floor of the estimate and doubles)
+    // (the copy path keeps the pool's 1/12 as a floor of the estimate too, and doubles)
     const long long step = h->vmm ? h->recent_growth() : std::max<long long>(h->recent_growth(), h->t.max_blocks / 12);
-    const long long need = used + 3 * step;
+    const long long need = used + std::max<long long>(3 * step, 2 * r.listed + step);
     if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, pool_target(h, need + step)));
     while ((double)(used + 3 * h->recent_growth() + h->tomb_est) >= h->max_load * (double)h->map_size)
         TSDF_TRY(grow_table(h));
@@ -828,7 +844,7 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
         launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
         TSDF_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
-                           (PoolReport*)nullptr, -1ll);
+                           (PoolReport*)nullptr, -1ll, (const unsigned*)nullptr);
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(read_state(h));
     }
@@ -858,7 +874,9 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         TSDF_HIP(hipMalloc(&h->d_res, sizeof(int) * kSets * (size_t)B.n_bricks));
     }
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
-    const int gc_full = h->t.owned ? (h->t.n_owned + 63) / 64 : (int)B.cull_grid_fused();
+    // (a shard that owns no brick -- more shards than bricks -- still runs one cull workgroup, which
+    // lists nothing, like the in-line path's max(1, ...))
+    const int gc_full = h->t.owned ? std::max(1, (h->t.n_owned + 63) / 64) : (int)B.cull_grid_fused();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;
@@ -982,7 +1000,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         TSDF_HIP(hipGetLastError());
         TSDF_TRY(B.prof.end(B.stream, e0));
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
-                           h->t.rb, h->seq++);
+                           h->t.rb, h->seq++, (const unsigned*)B.count);
         TSDF_HIP(hipGetLastError());
         B.frames += n;
         if (!sync) {
@@ -1065,7 +1083,7 @@ int insert_block_keys(tsdf_hash* h, const std::vector<unsigned long long>& keys,
                        B.pool, (const unsigned long long*)dkeys, (long long)nk, (int*)*dblk, (long long*)*dslot);
     TSDF_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
-                       (PoolReport*)nullptr, -1ll);
+                       (PoolReport*)nullptr, -1ll, (const unsigned*)nullptr);
     TSDF_HIP(hipGetLastError());
     return TSDF_OK;
 }
@@ -1199,6 +1217,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
         for (void* p : pool)
             if (p) (void)hipFree(p);
     }
+    for (const auto& r : h->retired_va) (void)hipMemAddressFree(r.first, r.second);
     if (h->h_rb) (void)hipHostFree(h->h_rb);
     delete h;
     return TSDF_OK;
@@ -1433,9 +1452,16 @@ int tsdf_hash_to_dense(tsdf_hash_t* h, tsdf_dense_t* d) {
     TSDF_TRY(hash_flush(h));
     TSDF_TRY(tsdf_dense_sync(d));  // (runs the dense handle's deferred frames first)
     Base& D = *dense_base(d);
+    // the same lattice: dims, contiguous columns, origin, voxel size and truncation (a handle with
+    // other bounds but equal dims would be filled with a misplaced volume)
+    bool same = D.vol.xstride == kBrickEdge && D.vol.xodd == kBrickEdge && D.vol.vs == B.vol.vs &&
+                D.vol.trunc == B.vol.trunc;
     for (int a = 0; a < 3; ++a)
-        if (D.vol.dims[a] != B.vol.dims[a] || D.vol.off[a] != 0 || D.vol.xstride != kBrickEdge)
-            return set_error(TSDF_E_ARG, "the dense handle must be an unsharded volume of the hash's dims");
+        same = same && D.vol.dims[a] == B.vol.dims[a] && D.vol.off[a] == 0 && B.vol.off[a] == 0 &&
+               D.vol.origin[a] == B.vol.origin[a];
+    if (!same)
+        return set_error(TSDF_E_ARG, "the dense handle must be an unsharded volume of the hash's geometry "
+                                     "(dims, origin, voxel size, truncation)");
     if (D.device != B.device) return set_error(TSDF_E_ARG, "the handles live on different devices");
     TSDF_TRY(tsdf_dense_reset(d));  // (1, 0, 0) everywhere, then the live blocks' entries
     hipLaunchKernelGGL(k_to_bricks, dim3(4096), dim3(256), 0, B.stream, B.vol, h->t, B.pool, D.pool);

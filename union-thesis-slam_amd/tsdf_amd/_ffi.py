@@ -131,8 +131,10 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
-    lib.tsdf_last_error.argtypes = []
-    lib.tsdf_last_error.restype = ctypes.c_char_p
+    for name in ("tsdf_last_error", "tsdf_build_id"):
+        fn = getattr(lib, name)
+        fn.argtypes = []
+        fn.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -155,6 +157,11 @@ def ptr(a) -> ctypes.c_void_p | None:
     if not a.flags["C_CONTIGUOUS"]:
         raise ValueError("array must be C-contiguous")
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def build_id() -> str:
+    """The loaded library's build id (sha256 prefix of its sources, tsdf_build_id)."""
+    return load().tsdf_build_id().decode()
 
 
 def device_count() -> int:

@@ -267,7 +267,6 @@ class HashTable:
         return t, c
 
     def get_state(self, weight=True):
-        self.trim()
         shape = tuple(int(x) for x in self._vol_dim)
         t = np.empty(shape, np.float32)
         w = np.empty(shape, np.float32) if weight else None
@@ -280,7 +279,6 @@ class HashTable:
         filled on the device from the live blocks (tsdf_hash_to_dense: no host round trip)."""
         lo = np.asarray(self._vol_bounds, dtype=np.float64)[:, 0]
         bnds = np.stack([lo, lo + (np.asarray(self._vol_dim) - 0.5) * self._voxel_size], axis=1)  # same dims
-        self.trim()
         with contextlib.redirect_stdout(io.StringIO()):
             vol = grid_fusion.TSDFVolume(bnds, self._voxel_size, device=self.device)
         _ffi.call("tsdf_hash_to_dense", self._h, vol._h)
@@ -299,7 +297,10 @@ class HashTable:
         _ffi.call("tsdf_hash_sync", self._h)
 
     def trim(self):
-        """Hand the block pool's memory above the live blocks back (tsdf_hash_trim)."""
+        """Hand the block pool's memory above the live blocks back (tsdf_hash_trim: a compaction
+        into fresh mapped ranges, one device copy of the live state).  Explicit only -- exports
+        (get_volume / get_state / get_mesh) do not trim, so periodic extraction during a run does
+        not shrink a pool the next integrate must grow again."""
         _ffi.call("tsdf_hash_trim", self._h)
 
     def stats(self, reset=False):
