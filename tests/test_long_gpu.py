@@ -72,15 +72,28 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
     assert w.max() >= 500 and vol.stats()["list_errors"] == 0
 
 
-def test_config3_rank_shard_5000_frames_crosses_the_table_limit_naturally():
-    """config[3]'s sequence length on one rank: cyclic column shard 3 of 8 of 512^3 @ 2 cm
-    integrates 5000 frames of the bench trajectory (625 batches).  Weights pass the 4087 limit of
-    the LDS part of the reciprocal table by accumulation alone (no preload), so waves move to the
-    HBM table mid-run; the two rows holding the largest weights equal the oracle bit for bit."""
+def test_config3_rank_shard_10000_frames_full_sequence():
+    """config[3]'s whole sequence on one rank (BASELINE: 10k frames; the demo loop is
+    grid_demo1.py:76-87): cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 10,000 frames of
+    the bench trajectory (1250 batches through the pipelined launches).  Weights pass the 4087
+    limit of the LDS part of the reciprocal table by accumulation alone (no preload), so waves
+    move to the HBM table mid-run, and stay below the whole table's 65527.  The two rows holding
+    the largest weights equal the oracle bit for bit; the frames stay in HBM (15 GB) and reach
+    the host in chunks for the oracle."""
+    import torch
     from tsdf_amd import grid_fusion, scene, sharding
-    n = 5000
-    depth, rgb, poses = _frames_on_device(n)
+    n, chunk = 10000, 1000
     K = scene.intrinsics()
+    dev = torch.device("cuda", 0)
+    poses = scene.trajectory(n, seed=0, radius_frac=scene.BENCH_RING)
+    spheres = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
+    depth = torch.empty((n, 480, 640), dtype=torch.int16, device=dev)
+    rgb = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
+    for s in range(0, n, 50):
+        d, c = scene.render(poses[s:s + 50], spheres, seed=0, start=s, device=dev, depth_dtype=torch.int16)
+        depth[s:s + len(d)] = d
+        rgb[s:s + len(c)] = c
+    torch.cuda.synchronize()
     Tinv = np.linalg.inv(poses)
     bnds = np.array([[0.0, ROOM]] * 3)
     vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(3, 8))
@@ -89,19 +102,20 @@ def test_config3_rank_shard_5000_frames_crosses_the_table_limit_naturally():
     xi = sharding.columns(3, 8, 512)
     _, W, _ = vol.get_state()
     row_max = W.reshape(len(xi), -1).max(1)
-    assert row_max.max() > 4087  # crossed by accumulation
+    assert 4087 < row_max.max() < 65527
     pick = np.argsort(row_max)[-2:]  # the two rows with the largest weights
     rows = xi[np.sort(pick)]
     del W
     orc = O.OracleTSDFVolume(bnds.copy(), 0.02, x_index=rows)
-    dh = depth.cpu().numpy().view(np.uint16)
-    ch = rgb.cpu().numpy()
-    del depth, rgb
-    for f in range(n):
-        orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    for c0 in range(0, n, chunk):
+        dh = depth[c0:c0 + chunk].cpu().numpy().view(np.uint16)
+        ch = rgb[c0:c0 + chunk].cpu().numpy()
+        for f in range(len(dh)):
+            orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[c0 + f])
     t, w, c = vol.get_rows(np.searchsorted(xi, rows))
     assert _same(t, orc._tsdf_vol_cpu) and _same(w, orc._weight_vol_cpu) and _same(c, orc._color_vol_cpu)
     assert (w > 4087).sum() > 100 and vol.stats()["list_errors"] == 0
+    assert vol.stats()["frames"] == n
 
 
 @pytest.mark.parametrize("batched,w_lo,limit", [(False, 4078, 4087), (True, 4078, 4087),

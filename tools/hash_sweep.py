@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Voxel-hash load-factor sweep (BASELINE config[2]) on the fused launch: a
-power-of-two device table of 2^18 slots filled to load factors 0.1 .. 0.9 by the blocks of more
-and more frames (the bench ring first, then other camera rings), the resize policy lifted to 0.95
+power-of-two device table of 2^17 slots filled to load factors 0.1 .. 0.95 by the blocks of more
+and more frames (the bench ring first, then other camera rings), the resize policy lifted to 0.97
 (TSDF_HASH_MAX_LOAD) so the table keeps its size; at each load the steady pass re-integrates the
 same 64 bench frames (lookups only): frames/s, Mvoxel-updates/s, mean / max probe distance,
-displaced keys.  Also the 1024^3 @ 1 cm extent's cull cost (same frames, 2^22 buckets, 8x the
-bricks the cull walks).  Prints one JSON object.
+displaced keys.  Then the reference's own policy (resize at 0.75, hash_fusion.py:156-161,414-437)
+active on a 2^17 table through the whole run, so that double_table_size happens mid-run.  Also
+the 1024^3 @ 1 cm extent's cull cost (same frames, 2^22 buckets, 8x the bricks the cull walks).
+Prints one JSON object.
 
   python tools/hash_sweep.py [--frames 400]
 """
@@ -26,9 +28,9 @@ sys.path.insert(0, os.path.join(REPO, "union-thesis-slam_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=400)
-    ap.add_argument("--loads", default="0.1,0.25,0.5,0.6,0.7,0.75,0.8,0.85,0.9")
+    ap.add_argument("--loads", default="0.1,0.25,0.5,0.6,0.7,0.75,0.8,0.85,0.9,0.95")
     a = ap.parse_args()
-    os.environ["TSDF_HASH_MAX_LOAD"] = "0.95"
+    os.environ["TSDF_HASH_MAX_LOAD"] = "0.97"  # (read by tsdf_hash_create: per table)
     import torch
     from tsdf_amd import hash_fusion, scene
     dev = torch.device("cuda", 0)
@@ -60,11 +62,12 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             return hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), vs, cap, max_blocks=max_blocks)
 
-    # Load factor on the fused launch: a power-of-two device table of S = 2^18 slots (every table
+    # Load factor on the fused launch: a power-of-two device table of S = 2^17 slots (every table
     # the library builds is one) filled to each target load by the blocks of more and more frames
-    # (the bench ring, then other camera rings), the resize policy lifted; then the steady pass
-    # re-integrates the same 64 bench frames (their blocks exist: lookups only).
-    S = 1 << 18
+    # (the bench ring, then other camera rings: up to 192k blocks, so every load up to 0.95 is
+    # reachable), the resize policy lifted; then the steady pass re-integrates the same 64 bench
+    # frames (their blocks exist: lookups only).
+    S = 1 << 17
     rings = [scene.BENCH_RING, 0.30, 0.20, 0.36, 0.25, 0.12]
     probe_n = 64
 
@@ -125,6 +128,43 @@ def main():
         out.append(res)
         del ht
         torch.cuda.empty_cache()
+    # The reference's policy active: a 2^17 table, TSDF_HASH_MAX_LOAD unset (0.75), the bench's 1000
+    # frames asynchronously and then synchronously per batch of 8 (the drop-in's checks): the table
+    # doubles when live keys reach 0.75 of it, mid-run, as double_table_size does
+    os.environ.pop("TSDF_HASH_MAX_LOAD", None)
+    policy = {}
+    for mode in ("async", "sync_per_batch"):
+        ht = table(0.02, S, 1 << 15)
+        caps = [int(ht.info()["capacity"])]
+        ht.stats(reset=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if mode == "async":
+            ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=False)
+        else:
+            for f0 in range(0, F, 8):
+                ht.integrate_batch(depth[f0].data_ptr(), rgb[f0].data_ptr(), K, Tinv[f0:f0 + 8], hw=(480, 640),
+                                   device_ptrs=True, sync=True)
+                c = int(ht.info()["capacity"]) if f0 % 64 == 0 else caps[-1]
+                if c != caps[-1]:
+                    caps.append(c)
+        ht.sync()
+        dt = time.perf_counter() - t0
+        st = ht.stats()
+        info = ht.info()
+        if st["bricks_skipped"] and mode == "async":
+            raise RuntimeError("bricks skipped")
+        if info["capacity"] != caps[-1]:
+            caps.append(int(info["capacity"]))
+        policy[mode] = {"frames_per_s": round(F / dt, 1), "table_size_start": S, "table_size_end": int(info["capacity"]),
+                        "table_sizes_seen": caps, "doublings": int(round(math.log2(info["capacity"] / S))),
+                        "blocks_live": int(info["used"]), "load_factor_end": round(info["used"] / info["capacity"], 4),
+                        "mean_probe": round(st["probe_steps"] / max(1, st["lookups"]), 3),
+                        "max_probe": int(st["probe_max"])}
+        print(json.dumps({"policy": policy}), file=sys.stderr, flush=True)
+        del ht
+        torch.cuda.empty_cache()
+    os.environ["TSDF_HASH_MAX_LOAD"] = "0.97"
     # the reference's own table sizes (HashTable(map_size=1000000), hash_fusion.py:34; 2000000 in
     # hash_demo1.py:110) against 2^22: the device table takes the next power of two of slots, so
     # every size runs the fused launch; steady pass over the same frames after an allocating pass
@@ -153,7 +193,8 @@ def main():
         print(json.dumps(ext), file=sys.stderr, flush=True)
         del ht
         torch.cuda.empty_cache()
-    print(json.dumps({"sweep": out, "frames": F, "slots": S, "extent_cost": ext, "reference_sizes": sizes,
+    print(json.dumps({"sweep": out, "frames": F, "slots": S, "policy_0_75": policy, "extent_cost": ext,
+                      "reference_sizes": sizes,
                       "volume": "512^3 @ 2 cm extent, 8^3 blocks; steady pass = the first 64 bench-ring frames x 4",
                       "kernel": "k_fused_hash<0> (power-of-two device table, z-half waves)"}))
 

@@ -632,12 +632,15 @@ __device__ inline double dist_of(const Vol& v, double diff) { return fmin(div_rn
 // brick's claim word of the batch (res[b], reset to kResFree by the cull that listed the brick):
 //  * at item start the z-low wave looks the block up (no insert) and publishes the block or
 //    kResMissing; the z-high wave waits for it.  Both then run the frame loop like the dense grid:
-//    no probe state is live inside the loop, so the hash integrate fits the dense grid's 80 VGPRs;
-//  * a missing block is allocated only if a half really updates a voxel: that half runs the frames
-//    up to its first valid voxel (a dry pass), claims the word (kResMissing -> kResBusy), inserts,
-//    initialises the other half and the entry words, publishes block | kResNew (or kResFail when
-//    the table or pool is full) and re-runs its frames; the other half, if it needs the block
-//    too, waits for the publication.  A claimer never waits, so every wait ends.
+//    no probe state is live inside the loop, so the hash integrate fits the dense grid's registers;
+//  * a missing block's voxels hold the fresh state (tsdf 1, weight 0, colour 0) -- exactly what
+//    the registers start with -- so a half runs its frames without the block, and only a half
+//    that updated a voxel needs one at the end: it claims the word (kResMissing -> kResBusy),
+//    inserts, initialises the other half and the entry words, publishes block | kResNew (or
+//    kResFail when the table or pool is full) and stores; the other half, if it updated a voxel
+//    too, waits for the publication and stores.  A claimer never waits, so every wait ends.  (No
+//    brick of a batch is listed twice and nothing else inserts during a launch, so a block missing
+//    at item start stays missing until one of its own halves inserts it.)
 // Both waves share a workgroup, so workgroup-scope ordering suffices (agent scope would write
 // back and invalidate the XCD's L2 at every claim).
 constexpr int kResFree = -1, kResBusy = -2, kResFail = -3, kResMissing = -4;
@@ -699,8 +702,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
     typename std::conditional<HASH, int, long long>::type blk = -1;
     bool is_new = false;
+    [[maybe_unused]] int* const rp = kHalfHash ? res + b : nullptr;
     if constexpr (kHalfHash) {
-        int* const rp = res + b;
         int cur;
         if (zoff == 0) {  // the z-low wave looks the block up for both halves
             long long slot = 0, probe = 0;
@@ -716,72 +719,13 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         } else {
             cur = res_wait(rp, kResFree);
         }
-        if (cur >= 0) {  // found, or (z-high wave) already inserted by its sibling
-            blk = cur & (kResNew - 1);
-            is_new = (cur & kResNew) != 0;
-        } else {  // missing: a dry pass up to this half's first valid voxel decides whether it needs one
-            bool need = false;
-            for (int fi = 0; fi < bt.n && !need; ++fi) {
-                if (!((fmask >> fi) & 1u)) continue;
-                unsigned cpx[NZ];
-                double diff[NZ];
-                bool okv[NZ], any = false;
-                project_part<DK, CK, NZ>(v, bt.f[fi], px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
-#pragma unroll
-                for (int k = 0; k < NZ; ++k) any |= okv[k];
-                need = __ballot(any) != 0;
+        if (cur >= 0) {  // found: a block of an earlier launch
+            if (cur >= tab.max_blocks) {  // never: a table value is one of the pool's blocks
+                if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
+                return;
             }
-            if (!need) return;  // no frame of the batch updates this half
-            cur = res_load(rp);
-            bool claimer = false;
-            if (cur == kResMissing) {
-                int old = kResMissing;
-                if (lane == 0)
-                    __hip_atomic_compare_exchange_strong(rp, &old, kResBusy, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-                old = __shfl(old, 0);
-                claimer = old == kResMissing;
-                cur = old;
-            }
-            if (claimer) {
-                long long slot = 0, probe = 0;
-                const int r = table_find_or_insert(tab, pack_key(bx, by, bz),
-                                                   ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits), true, is_new,
-                                                   slot, probe);
-                if (r < 0) {  // no space: the brick waits for the host's re-run (nothing written)
-                    if (lane == 0) {
-                        const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
-                        if ((long long)o < tab.overflow_cap) tab.overflow[o] = entry;
-                        atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
-                    }
-                    res_publish(rp, kResFail);
-                    return;
-                }
-                if (is_new) {  // the other half and every entry word start fresh too
-                    const size_t pb = (size_t)r * kBrickVox + (size_t)lane * kBrickEdge + (4 - zoff);
-                    *(float4*)(pool.weight + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    *(float4*)(pool.tsdf + pb) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-                    *(float4*)(pool.color + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    if (lane < kBrickEdge) coh_store(tab.occ + (size_t)r * kBrickEdge + lane, 0ull);
-                }
-                cur = r | (is_new ? kResNew : 0);
-                res_publish(rp, cur);
-                if (lane == 0) {
-                    atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
-                    atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
-                    if (is_new) atomicAdd(&s_stat[ST_ALLOC], 1ull);
-                }
-            } else {
-                cur = res_wait(rp, kResBusy);
-                if (cur == kResFail) return;
-            }
-            blk = cur & (kResNew - 1);
-            is_new = (cur & kResNew) != 0;
-        }
-        if (blk >= tab.max_blocks) {  // never: a published block is one of this launch's pool
-            if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
-            return;
-        }
+            blk = cur;
+        }  // else missing: blk stays -1 and the frame loop starts from the fresh state (below)
     }
     float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
@@ -796,8 +740,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     constexpr int kH = NZ / 4;
     bool loaded[kH];
 #pragma unroll
-    for (int h = 0; h < kH; ++h) loaded[h] = kHalfHash && is_new;
-    unsigned touched = 0;  // voxels updated by any frame of the batch (entry bits, hash)
+    for (int h = 0; h < kH; ++h) loaded[h] = kHalfHash && blk < 0;  // a missing hash block: fresh state
+    // voxels updated by any frame of the batch (entry bits, hash): per z-step, the OR of the
+    // step masks' ballots -- scalar registers and scalar ORs, no per-lane VGPR bit field
+    unsigned long long touched[HASH ? NZ : 1] = {};
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
     bool w_table = true;   // ... < kRcpBig
     bool c_canon = true;   // all loaded colours are canonical (canon_color)
@@ -897,7 +843,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         for (int h = 0; h < kH; ++h) loaded[h] |= need[h];
         if (HASH) {
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) touched |= okv[k] ? 1u << k : 0u;
+            for (int k = 0; k < NZ; ++k) touched[k] |= __ballot(okv[k]);
         }
 #pragma unroll
         for (int k = 0; k < NZ; ++k) nupd += (unsigned)__popcll(__ballot(okv[k]));  // (wave total, scalar)
@@ -1017,8 +963,63 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         atomicAdd(&s_stat[ST_LOOKUPS], (unsigned long long)d_valid);
     }
 #endif
-    if (blk < 0) return;  // no frame of the batch updated this brick
-    if (kHalfHash && __ballot(touched != 0) == 0) return;  // (its block was looked up in advance)
+    if constexpr (kHalfHash) {
+        unsigned long long any = 0;
+#pragma unroll
+        for (int k = 0; k < NZ; ++k) any |= touched[k];
+        if (any == 0) return;  // this half updated nothing (its block, if any, was looked up in advance)
+        if (blk < 0) {  // missing block, and this half updated a voxel: claim it or wait for the claimer
+            int cur = res_load(rp), old = kResMissing;
+            if (cur == kResMissing) {
+                if (lane == 0)
+                    __hip_atomic_compare_exchange_strong(rp, &old, kResBusy, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __shfl(old, 0);
+                cur = old;
+            }
+            if (old == kResMissing && cur == kResMissing) {  // this wave claimed the word
+                long long slot = 0, probe = 0;
+                const int r = table_find_or_insert(tab, pack_key(bx, by, bz),
+                                                   ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits), true,
+                                                   is_new, slot, probe);
+                if (r < 0 || !is_new) {
+                    // r < 0: no space -- the brick waits for the host's exact re-run (nothing written);
+                    // !is_new never happens (the block was missing and only its halves insert it)
+                    if (lane == 0) {
+                        if (r < 0) {
+                            const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
+                            if ((long long)o < tab.overflow_cap) tab.overflow[o] = entry;
+                            atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
+                        } else {
+                            atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
+                        }
+                    }
+                    res_publish(rp, kResFail);
+                    return;
+                }
+                // the other half and every entry word start fresh too
+                const size_t pb = (size_t)r * kBrickVox + (size_t)lane * kBrickEdge + (4 - zoff);
+                *(float4*)(pool.weight + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                *(float4*)(pool.tsdf + pb) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                *(float4*)(pool.color + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (lane < kBrickEdge) coh_store(tab.occ + (size_t)r * kBrickEdge + lane, 0ull);
+                res_publish(rp, r | kResNew);
+                if (lane == 0) {
+                    atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
+                    atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
+                    atomicAdd(&s_stat[ST_ALLOC], 1ull);
+                }
+                blk = r;
+            } else {
+                cur = res_wait(rp, kResBusy);
+                if (cur == kResFail) return;
+                blk = cur & (kResNew - 1);
+            }
+            is_new = true;
+        }
+    } else if (blk < 0) {
+        return;  // no frame of the batch updated this brick
+    }
 
     // phase 6: store the changed halves once (a new hash block is written whole: its init)
     const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
@@ -1033,8 +1034,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         unsigned long long mine = 0;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            const unsigned long long m = __ballot((touched >> k) & 1u);
-            if (lane == k) mine = m;
+            if (lane == k) mine = touched[k];
         }
         if (lane < NZ) {
             unsigned long long* o = tab.occ + (size_t)blk * kBrickEdge + zoff + lane;

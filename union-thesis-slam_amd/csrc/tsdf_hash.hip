@@ -147,7 +147,12 @@ struct tsdf_hash {
         bool on = false;
         Batch bt;
         int dk = 0, ck = 0;
+        long long seq = -1;  // its integrate launch (the pool report the settle reads)
     } pend;
+    // Fused calls rotate the buffer sets across calls (batch j of a call uses set (j + set_rot) %
+    // kSets), so a deferred batch's prep / cull can be issued while the previous batch is still
+    // pending: its buffers stay intact for an exact re-run.
+    int set_rot = 0;
     bool fused = true;  // three-stage launches (k_fused_hash) when a call allows them
     // Asynchronous calls (TSDF_ASYNC): every allocating launch reports its pool state into
     // page-locked host memory (PoolReport, slot seq % kReports); before issuing launch s the host
@@ -860,13 +865,20 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
 // Internal flag of hash_run: a synchronous call of at most one batch whose overflow check
 // (hash_after_batch + ensure_room) is left to the next call on the handle (hash_settle).
 constexpr int kCheckLater = 1 << 30;
+int hash_settle(tsdf_hash* h);
 
 int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* color, int H, int W,
                    const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     const bool sync = !(flags & TSDF_ASYNC);
     const bool later = sync && (flags & kCheckLater) && n_frames <= kMaxBatch;
+    // a pending batch's exact re-run reads its buffer set and staging slot: settle it first if this
+    // call reallocates per-batch buffers (first fused call, another image size)
+    if (h->pend.on && !(B.n_sets >= kSets && B.pyr_H == H && B.pyr_W == W && B.stage_fits(dk, TSDF_COLOR_RGB8, H, W)))
+        TSDF_TRY(hash_settle(h));
     TSDF_TRY(B.use_sets(kSets));
+    const int rot = h->set_rot;
+    const auto set_of = [rot](int j) { return (j + rot) % kSets; };
     const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
     if (!h->d_res) {  // each word is written by the cull that lists its brick before an integrate reads it
         if (h->t.max_blocks >= kResNew || B.n_bricks >= (1ll << 31) / kSets)
@@ -878,12 +890,13 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     // lists nothing, like the in-line path's max(1, ...))
     const int gc_full = h->t.owned ? std::max(1, (h->t.n_owned + 63) / 64) : (int)B.cull_grid_fused();
     Batch bts[kSets];
+    h->set_rot = (rot + nb) % kSets;
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;
         if (jp < nb) {
             const int f0 = jp * kMaxBatch;
             const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
-            B.use_set(jp % kSets);
+            B.use_set(set_of(jp));
             // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
             TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, dk, color, TSDF_COLOR_RGB8, H, W,
                                      K, Tinv, nullptr, 1.0, flags, f0, n, jp % kSlots));
@@ -900,19 +913,23 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         sg.ptx = (W + 63) / 64;
         sg.pty = (H + 63) / 64;
         if (has_i) {
-            sg.list_i = B.list_set[L % kSets];
-            sg.count_i = B.count_set[L % kSets];
-            sg.res_i = h->d_res + (size_t)(L % kSets) * B.n_bricks;
+            sg.list_i = B.list_set[set_of(L)];
+            sg.count_i = B.count_set[set_of(L)];
+            sg.res_i = h->d_res + (size_t)set_of(L) * B.n_bricks;
         }
         if (has_c) {
-            sg.list_c = B.list_set[(L + 1) % kSets];
-            sg.count_c = B.count_set[(L + 1) % kSets];
-            sg.res_c = h->d_res + (size_t)((L + 1) % kSets) * B.n_bricks;
+            sg.list_c = B.list_set[set_of(L + 1)];
+            sg.count_c = B.count_set[set_of(L + 1)];
+            sg.res_c = h->d_res + (size_t)set_of(L + 1) * B.n_bricks;
         }
-        if (has_p) sg.count_p = B.count_set[jp % kSets];
+        if (has_p) sg.count_p = B.count_set[set_of(jp)];
         const long long grid = (long long)sg.gi + sg.gc + (has_p ? (long long)sg.ptx * sg.pty * bp.n : 0);
         if (grid >= (1ll << 31)) return set_error(TSDF_E_ARG, "fused grid too large");
         if (has_i) {
+            // the previous deferred batch's overflow check (its report; an exact re-run if it
+            // skipped bricks) comes before this batch's integrate -- after this call's own ingest,
+            // prep and cull were issued, so they overlap the previous batch on the GPU
+            if (h->pend.on) TSDF_TRY(hash_settle(h));
             if (!sync) TSDF_TRY(async_room(h, h->seq));
             sg.seq = h->seq++;
         } else {
@@ -935,6 +952,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
             h->pend.bt = bi;
             h->pend.dk = dk;
             h->pend.ck = TSDF_COLOR_RGB8;
+            h->pend.seq = sg.seq;
             h->pend.on = true;
         } else if (sync) {
             TSDF_TRY(hash_after_batch(h, bi, dk, TSDF_COLOR_RGB8));
@@ -976,6 +994,7 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     if (fused && (flags & TSDF_DEVICE_PTRS))
         fused = (uintptr_t)depth % (dk == TSDF_DEPTH_U16_MM ? 8 : 16) == 0 && (uintptr_t)color % 4 == 0 &&
                 ((size_t)H * W) % 4 == 0;
+    if (!fused && h->pend.on) TSDF_TRY(hash_settle(h));  // (the in-line path checks each batch at once)
     if (fused) {
         TSDF_TRY(hash_run_fused(h, n_frames, depth, dk, color, H, W, K, Tinv, flags));
         TSDF_TRY(guard.finish());
@@ -1019,9 +1038,22 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
 // The pending deferred batch's overflow check: grow the table / pool and re-run its skipped
 // bricks exactly (hash_after_batch), then the load-factor policy.  Nothing has been launched on
 // the handle since that batch, so its frames and prepped buffers are intact.
+// The batch's integrate launch reported its pool state into page-locked host memory (PoolReport):
+// without overflow the check is that report alone -- no stream synchronisation, no device read --
+// and the load-factor policy on its counts; with overflow, the exact synchronous re-run.
 int hash_settle(tsdf_hash* h) {
     if (!h->pend.on) return TSDF_OK;
     h->pend.on = false;
+    PoolReport r;
+    TSDF_TRY(wait_report(h, h->pend.seq, &r));
+    if (r.n_overflow == 0) {
+        h->host_st.pool_top = r.pool_top;
+        h->host_st.free_count = r.free_count;
+        h->host_st.n_overflow = 0;
+        h->host_st.cursor = 0;
+        h->host_st.tombs = h->tomb_est;  // (only remove() adds tombstones: a synchronous call)
+        return ensure_room(h, true);
+    }
     TSDF_TRY(hash_after_batch(h, h->pend.bt, h->pend.dk, h->pend.ck));
     TSDF_TRY(ensure_room(h, true));
     return TSDF_OK;
@@ -1034,7 +1066,9 @@ int hash_settle(tsdf_hash* h) {
 // bricks re-run exactly before any later frame is integrated.
 int hash_flush(tsdf_hash* h, bool wait = true) {
     Base& B = h->b;
-    TSDF_TRY(hash_settle(h));
+    // (wait = false: a pending batch is settled inside hash_run, right before this batch's
+    // integrate launch, once this batch's ingest / prep / cull are queued behind it)
+    if (wait || B.dfr.n == 0) TSDF_TRY(hash_settle(h));
     if (B.dfr.n == 0) return TSDF_OK;
     const Base::Deferred d = B.dfr;
     B.dfr.n = 0;
