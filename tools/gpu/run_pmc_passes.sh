@@ -1,4 +1,5 @@
-# The two PMC traffic passes of tools/gpu/run_profile.sh and the SQ pass, without the rocprof stats run.
+# The two PMC traffic passes (FETCH_SIZE, WRITE_SIZE; --kernel-trace only beside --pmc) and the SQ
+# pass, each a dense-only bench at the driver's window (--steps 20 --warmup 5).
 set -o pipefail
 R=$(pwd)
 O="$R/gpurun_out/profile"
@@ -7,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for pass in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/pmc_$i -o pmc -- python "$R/bench.py" --steps 50 --warmup 5 --no-hash --no-cpu --no-profile --no-ingest --no-dropin --no-mesh --no-lounge > "$O/pmc_$pass.json" 2> "$O/pmc_$pass.err" || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/pmc_$i -o pmc -- python "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-hash --no-cpu --no-profile --no-ingest --no-dropin --no-mesh --no-lounge > "$O/pmc_$pass.json" 2> "$O/pmc_$pass.err" || exit $?
   f=$(find /tmp/pmc_$i -name "*counter_collection.csv" | head -1)
   [ -n "$f" ] && grep -E "tsdf|Counter_Name" "$f" > "$O/pmc_$pass.csv"
 done

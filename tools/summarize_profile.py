@@ -1,8 +1,17 @@
 #!/usr/bin/env python3
-"""Turn gpurun_out/profile/ (tools/gpu/run_profile.sh) into the committed profile summaries:
-  profiles/<tag>_kernel_stats.csv      rocprofv3 --kernel-trace --stats of the default bench
+"""Turn gpurun_out/profile/ and gpurun_out/pmc_sq/ (tools/gpu/run_round_prof.sh) into the committed
+profile summaries, each stamped with the build id of the library that ran (tsdf_build_id, from the
+bench line printed under the profiler):
+  profiles/<tag>_kernel_stats.csv      rocprofv3 --kernel-trace --stats of the driver's bench command
   profiles/<tag>_bench.json            the bench line printed under that profiler
-  profiles/pmc_integrate_<tag>.json    HBM traffic per integrate launch from FETCH_SIZE/WRITE_SIZE
+  profiles/<tag>_timed_launches.csv    the trace rows of the 20 timed integrate launches, and their
+                                       average (must agree with the line's roofline.kernel_avg_us)
+  profiles/pmc_integrate_<tag>.json    HBM traffic per timed integrate launch (FETCH_SIZE/WRITE_SIZE)
+  profiles/pmc_sq_<tag>.json           SQ issue counters per timed integrate launch
+
+The timed launches: bench.py's warm-up call of W batches issues W + 2 pipelined launches of
+k_fused<true, 4, 0>, the timed call 2 + K of them, the last K of which integrate; so they are the
+launches W + 4 .. W + 3 + K of that kernel in dispatch order (the ingest leg's launches follow).
 
 FETCH_SIZE/WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
 coalesced read (MI355X_MICROARCH.md, HBM section); the integrate kernel's HBM reads are its
@@ -17,16 +26,30 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "tsdf::k_fused<true, 4, 0>"
+W, K = 5, 20  # the driver's --warmup / --steps
 
 
-def per_kernel(path, counter):
-    out = {}
+def bench_line(path):
+    with open(path) as f:
+        return json.loads([l for l in f if l.startswith("{")][-1])
+
+
+def timed(rows_by_dispatch):
+    """rows_by_dispatch: [(dispatch_id, row)] of KERNEL in dispatch order -> the K timed launches."""
+    rows = sorted(rows_by_dispatch, key=lambda r: r[0])
+    return rows[W + 4:W + 4 + K]
+
+
+def pmc_timed(path, counter):
+    per = {}
     for row in csv.DictReader(open(path)):
-        if row["Counter_Name"] != counter:
+        if row["Counter_Name"] != counter or not row["Kernel_Name"].startswith(KERNEL):
             continue
-        k = row["Kernel_Name"].split("(")[0].replace("void ", "")
-        out.setdefault(k, []).append(float(row["Counter_Value"]))
-    return out
+        d = int(row["Dispatch_Id"])
+        per[d] = per.get(d, 0.0) + float(row["Counter_Value"])  # (summed over dimensions / XCDs)
+    t = timed(list(per.items()))
+    return [v for _, v in t]
 
 
 def main(tag):
@@ -34,55 +57,60 @@ def main(tag):
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
-    with open(os.path.join(src, "bench_under_rocprof.json")) as f:
-        line = [l for l in f if l.startswith("{")][-1]
+    line = bench_line(os.path.join(src, "bench_under_rocprof.json"))
     with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
-        f.write(line)
-    fetch = per_kernel(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
+        f.write(json.dumps(line) + "\n")
+    bid = line.get("build_id")
+    # the timed launches' trace rows
+    trace = [r for r in csv.DictReader(open(os.path.join(src, "kernel_trace_tsdf.csv")))
+             if r["Kernel_Name"].startswith(KERNEL)]
+    t = timed([(int(r["Dispatch_Id"]), r) for r in trace])
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for _, r in t]
+    with open(os.path.join(dst, f"{tag}_timed_launches.csv"), "w") as f:
+        f.write(f"# {KERNEL}: the {K} timed integrate launches of bench.py --gpus 1 --steps {K} --warmup {W} "
+                f"under rocprofv3 (build {bid}); average {statistics.mean(durs):.2f} us, the line's "
+                f"roofline.kernel_avg_us {line['roofline']['kernel_avg_us']} (HIP events)\n")
+        f.write("dispatch_id,start_ns,end_ns,duration_us\n")
+        for (d, r), us in zip(t, durs):
+            f.write(f"{d},{r['Start_Timestamp']},{r['End_Timestamp']},{us:.2f}\n")
+    fetch = pmc_timed(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
+    write = pmc_timed(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
+    pl = bench_line(os.path.join(src, "pmc_FETCH_SIZE.json"))
     sys.path.insert(0, REPO)
     import bench
-    summary = {"note": __doc__.strip().splitlines()[-4:], "kernels": {}, "workload": bench.WORKLOAD}
-    for k in sorted(set(fetch) | set(write)):
-        fk = statistics.median(fetch.get(k, [0.0])) * 1024.0
-        wk = statistics.median(write.get(k, [0.0])) * 1024.0
-        summary["kernels"][k] = {"fetch_bytes_raw": fk, "fetch_bytes_corrected": 2 * fk,
-                                 "write_bytes": wk, "hbm_bytes": 2 * fk + wk,
-                                 "launches_sampled": len(fetch.get(k, []))}
-        # the dense integrate launch: k_fused (pipelined; also culls k+1 / preps k+2) or the
-        # in-line k_integrate<false, ...>
-        if k.startswith("tsdf::k_fused<true") or (k.startswith("tsdf::k_integrate<false")
-                                                  and "kernel" not in summary):
-            summary["hbm_bytes_per_launch"] = round(2 * fk + wk)
-            summary["kernel"] = k
+    fk = statistics.median(fetch) * 1024.0
+    wk = statistics.median(write) * 1024.0
+    summary = {"kernel": KERNEL, "build_id": pl.get("build_id"), "workload": bench.WORKLOAD,
+               "window": f"bench.py --gpus 1 --steps {K} --warmup {W}: the {K} timed launches (median)",
+               "launches_sampled": [len(fetch), len(write)],
+               "fetch_bytes_raw": fk, "fetch_bytes_corrected": 2 * fk, "write_bytes": wk,
+               "hbm_bytes_per_launch": round(2 * fk + wk),
+               "timed_launch_avg_us_under_rocprof": round(statistics.mean(durs), 2),
+               "note": __doc__.strip().splitlines()[-4:]}
     with open(os.path.join(dst, f"pmc_integrate_{tag}.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
 
 
-def sq(tag="r02"):
+def sq(tag):
     """gpurun_out/pmc_sq/pmc_sq.csv (tools/gpu/run_pmc_sq.sh) -> profiles/pmc_sq_<tag>.json: SQ
-    counters per launch of the dense integrate launch and its VALU-busy fraction."""
-    src = os.path.join(REPO, "gpurun_out", "pmc_sq", "pmc_sq.csv")
-    per = {}
-    kernel = None
-    for row in csv.DictReader(open(src)):
-        k = row["Kernel_Name"].split("(")[0].replace("void ", "")
-        if not k.startswith("tsdf::k_fused<true"):
-            continue
-        kernel = k
-        per.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    med = {c: statistics.median(v) for c, v in sorted(per.items())}
+    counters per timed launch of the dense integrate launch and its VALU-busy fraction."""
+    src = os.path.join(REPO, "gpurun_out", "pmc_sq")
+    names = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+             "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+    med = {c: statistics.median(pmc_timed(os.path.join(src, "pmc_sq.csv"), c)) for c in names}
+    pl = bench_line(os.path.join(src, "bench.json"))
     sys.path.insert(0, REPO)
     import bench
-    out = {"kernel": kernel, "median_per_launch": med,
+    out = {"kernel": KERNEL, "build_id": pl.get("build_id"), "median_per_launch": med,
            # SQ_* cycle counters count quad-cycles; 1024 SIMDs, GRBM_GUI_ACTIVE summed over 8 XCDs
            "valu_busy_per_simd": round(med["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * med["GRBM_GUI_ACTIVE"] / 8), 3),
            "valu_per_vmem": round(med["SQ_INSTS_VALU"] / med["SQ_INSTS_VMEM"], 1),
+           "wait_any_frac": round(med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"], 3),
            "workload": bench.WORKLOAD,
-           "note": "rocprofv3 --pmc pass (tools/gpu/run_pmc_sq.sh, 50 steps); SQ_* cycle counters in "
-                   "quad-cycles per MI355X_MICROARCH.md; busy = ACTIVE_INST_VALU x 4 / (1024 SIMDs x "
-                   "GRBM_GUI_ACTIVE / 8 XCDs)"}
+           "window": f"bench.py --gpus 1 --steps {K} --warmup {W}: the {K} timed launches (median)",
+           "note": "rocprofv3 --pmc pass (tools/gpu/run_pmc_sq.sh); SQ_* cycle counters in quad-cycles per "
+                   "MI355X_MICROARCH.md; busy = ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)"}
     with open(os.path.join(REPO, "profiles", f"pmc_sq_{tag}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
