@@ -704,8 +704,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     bool is_new = false;
     [[maybe_unused]] int* const rp = kHalfHash ? res + b : nullptr;
     if constexpr (kHalfHash) {
-        int cur;
-        if (zoff == 0) {  // the z-low wave looks the block up for both halves
+        int cur = res_load(rp);  // the cull's lookup (or kResFree), written by the previous launch
+        if (cur >= 0) {
+        } else if (zoff == 0) {  // not found by the cull: the z-low wave looks again, for both halves
             long long slot = 0, probe = 0;
             const int r = table_find_or_insert(tab, pack_key(bx, by, bz), ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits),
                                                false, is_new, slot, probe);
@@ -1061,9 +1062,35 @@ constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 
 
 // Wave-level append of the kept bricks (lane: brick e, its frame mask) to the sub-list of their cost
 // class (frames kept): one atomicAdd per class with survivors.
+// The fused hash launch's cull also looks every kept brick's block up (one lane per brick, a
+// linear probe of the power-of-two table: about one slot at the bench's load factors) and leaves
+// the block in the brick's claim word, so that the integrate's waves start at once; a brick not
+// found there (a new one -- or one the integrate of the previous batch, running in the same launch,
+// inserts only now) gets kResFree and is looked up again by its z-low wave (integrate_brick).
+__device__ inline int cull_lookup(const Vol& v, const Table& t, unsigned e, unsigned long long* s_stat) {
+    const int nb12 = v.nb[1] * v.nb[2];
+    const int bx = (int)e / nb12, r = (int)e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
+    const unsigned long long key = pack_key(bx, by, bz);
+    const long long mask = t.capacity - 1;
+    long long s = ref_hash<true>(bx, by, bz, t.capacity, t.int_bits);
+    for (long long n = 0; n < t.capacity; ++n) {
+        const unsigned long long k = coh_load(&t.keys[s]);
+        if (k == key) {
+            const int blk = coh_load(&t.vals[s]);
+            atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
+            atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
+            atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
+            return (blk >= 0 && blk < t.max_blocks) ? blk : kResFree;
+        }
+        if (k == kEmpty) break;
+        s = (s + 1) & mask;
+    }
+    return kResFree;
+}
+
 template <bool HASH>
 __device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* count, unsigned long long* s_stat,
-                                   int* res, unsigned e, unsigned fmask) {
+                                   int* res, unsigned e, unsigned fmask, const Table* tab = nullptr) {
     const int lane = lane_id();
     const int cls = __popc(fmask);
     const unsigned long long any = __ballot(cls != 0);
@@ -1082,7 +1109,8 @@ __device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* 
     const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
     if (cls && base + rank < nbk) {
         list[(size_t)(cls - 1) * nbk + base + rank] = (ListEntry)e | ((ListEntry)fmask << 32);
-        if (HASH && res) res[e] = kResFree;  // the brick's claim word for this batch
+        // the brick's claim word for this batch: its block when the cull looked it up
+        if (HASH && res) res[e] = tab ? cull_lookup(v, *tab, e, s_stat) : kResFree;
     }
 }
 
@@ -1134,7 +1162,7 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
         const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
         append_kept<HASH>(v, list, count, s_stat, res, (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz),
-                          s_mask[wave * 64 + lane]);
+                          s_mask[wave * 64 + lane], P2 ? &tab : nullptr);
     }
     __syncthreads();
     flush_stats(s_stat, stats);
@@ -1163,7 +1191,7 @@ __device__ inline void cull_owned(const Vol& v, const Batch& bt, const Table& ta
         if (have && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
     }
     __syncthreads();
-    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u);
+    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u, &tab);
     __syncthreads();
     flush_stats(s_stat, stats);
 }

@@ -231,10 +231,16 @@ struct InfoDev {
     unsigned long long used, tomb, displaced, max_probe, entries;
 };
 
-__global__ void k_fill_keys(unsigned long long* k, long long n) {
+// Empty slots hold value -1 (invariant: a slot's value is -1 whenever its key is empty or a
+// tombstone), so a reader that sees a key inserted concurrently -- the CAS of the key comes before
+// the store of its value -- reads -1, never a stale block (the fused hash launch's cull looks
+// blocks up while the integrate of the batch before inserts: cull_lookup).
+__global__ void k_fill_keys(unsigned long long* k, int* vals, long long n) {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x)
+         i += (long long)gridDim.x * blockDim.x) {
         k[i] = kEmpty;
+        vals[i] = -1;
+    }
 }
 
 // After each allocating launch: fold the launch's allocations into the pool state.
@@ -384,6 +390,7 @@ __global__ void k_free_empty(Table t, const unsigned long long* keys, long long 
     const long long blk = coh_load(&t.vals[s]);
     for (int k = 0; k < 8; ++k)
         if (coh_load(&t.occ[blk * 8 + k])) return;
+    coh_store(&t.vals[s], -1);  // (the empty-slot invariant, k_fill_keys)
     coh_store(&t.keys[s], kTomb);
     atomicAdd((unsigned long long*)&t.st->tombs, 1ull);
     const unsigned long long f = atomicAdd((unsigned long long*)&t.st->free_count, 1ull);
@@ -681,7 +688,7 @@ int resize_table(tsdf_hash* h, long long new_cap) {
     DevBufs fresh;
     TSDF_TRY(dev_alloc(fresh, &nt.keys, sizeof(unsigned long long) * new_cap));
     TSDF_TRY(dev_alloc(fresh, &nt.vals, sizeof(int) * new_cap));
-    hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, nt.keys, (long long)new_cap);
+    hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, nt.keys, nt.vals, (long long)new_cap);
     TSDF_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_rehash, dim3(2048), dim3(256), 0, B.stream, h->t, nt);
     TSDF_HIP(hipGetLastError());
@@ -1263,7 +1270,8 @@ int tsdf_hash_reset(tsdf_hash_t* h) {
     B.dfr.n = 0;  // deferred frames are dropped with the state
     h->pend.on = false;
     TSDF_HIP(hipSetDevice(B.device));
-    hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, h->t.keys, (long long)h->t.capacity);
+    hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, h->t.keys, h->t.vals,
+                       (long long)h->t.capacity);
     TSDF_HIP(hipGetLastError());
     TSDF_HIP(hipMemsetAsync(h->t.st, 0, sizeof(PoolState), B.stream));
     TSDF_HIP(hipMemsetAsync(B.stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, B.stream));
