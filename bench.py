@@ -76,6 +76,8 @@ def parse():
                     help="A/B: keep the resident depth as float64 metres (the f64-texel integrate)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: several ranks may share a GPU)")
+    ap.add_argument("--preheat-ms", type=float, default=0.0,
+                    help="untimed integrate work on the volume (then reset) before the warm-up steps")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)  # tests: ranks, no GPU
     return ap.parse_args()
 
@@ -340,6 +342,13 @@ def main():
         vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=gpu, shard=(rank, n))
     W, Ks = args.warmup, args.steps
     Wf, Kf = W * BATCH, Ks * BATCH
+    if args.preheat_ms > 0:
+        t_end = time.perf_counter() + args.preheat_ms / 1e3
+        f0 = 0
+        while time.perf_counter() < t_end:
+            run_timed(vol, depth, rgb, K, Tinv, f0, 20 * BATCH, F, sync, lambda: None, False)
+            f0 += 20 * BATCH
+        vol.reset()
     run_timed(vol, depth, rgb, K, Tinv, 0, Wf, F, sync, barrier, False)
     dt = run_timed(vol, depth, rgb, K, Tinv, Wf, Kf, F, sync, barrier, not args.no_profile)
     st = vol.stats()

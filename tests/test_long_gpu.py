@@ -72,6 +72,7 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
     assert w.max() >= 500 and vol.stats()["list_errors"] == 0
 
 
+@pytest.mark.timeout(400)
 def test_config3_rank_shard_10000_frames_full_sequence():
     """config[3]'s whole sequence on one rank (BASELINE: 10k frames; the demo loop is
     grid_demo1.py:76-87): cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 10,000 frames of

@@ -8,7 +8,7 @@ O="$R/gpurun_out/r04_ab1"
 mkdir -p "$O"
 export PYTHONPATH="$R/union-thesis-slam_amd"
 for rep in 1 2; do
-  for n in r4a r4b r4c r4d hotd; do
+  for n in r4a r4b r4c r4d hotd lazy expect; do
     TSDF_HIP_LIB=$R/abtest/lib$n.so timeout -k 10 300 python -u tools/gpu/ab_window.py 5 $n >> "$O/ab.jsonl" 2>> "$O/ab.err" || exit $?
   done
 done

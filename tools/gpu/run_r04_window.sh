@@ -16,5 +16,4 @@ ls -la "$O"
 cd "$R"
 # bench.py --gpus 2 on a one-GPU box: two ranks it launches itself, sharing the GPU over gloo
 timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-hash --no-cpu --no-dropin --no-lounge > "$O/bench_gpus2_gloo.json" 2> "$O/bench_gpus2_gloo.err" || exit $?
-timeout -k 10 600 python -u -m pytest tests/test_dropin_gpu.py tests/test_hash_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$O/tests_hash.log" 2>&1 || exit $?
-cd "$R" && bash tools/gpu/run_r04_ab1.sh
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$O/tests_hash.log" 2>&1 || exit $?

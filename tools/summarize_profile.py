@@ -44,7 +44,7 @@ def timed(rows_by_dispatch):
 def pmc_timed(path, counter):
     per = {}
     for row in csv.DictReader(open(path)):
-        if row["Counter_Name"] != counter or not row["Kernel_Name"].startswith(KERNEL):
+        if row["Counter_Name"] != counter or KERNEL not in row["Kernel_Name"]:
             continue
         d = int(row["Dispatch_Id"])
         per[d] = per.get(d, 0.0) + float(row["Counter_Value"])  # (summed over dimensions / XCDs)
@@ -63,7 +63,7 @@ def main(tag):
     bid = line.get("build_id")
     # the timed launches' trace rows
     trace = [r for r in csv.DictReader(open(os.path.join(src, "kernel_trace_tsdf.csv")))
-             if r["Kernel_Name"].startswith(KERNEL)]
+             if KERNEL in r["Kernel_Name"]]
     t = timed([(int(r["Dispatch_Id"]), r) for r in trace])
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for _, r in t]
     with open(os.path.join(dst, f"{tag}_timed_launches.csv"), "w") as f:

@@ -720,13 +720,18 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         } else {
             cur = res_wait(rp, kResFree);
         }
-        if (cur >= 0) {  // found: a block of an earlier launch
-            if (cur >= tab.max_blocks) {  // never: a table value is one of the pool's blocks
+        if (cur >= 0) {
+            // found -- a block of an earlier launch, or (kResNew: a z-high wave that starts late) the
+            // block its z-low half already inserted, this half initialised to the fresh state before
+            // the publication this acquire-load saw
+            blk = cur & (kResNew - 1);
+            is_new = (cur & kResNew) != 0;
+            if (blk >= tab.max_blocks) {  // never: a table value is one of the pool's blocks
                 if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
                 return;
             }
-            blk = cur;
-        }  // else missing: blk stays -1 and the frame loop starts from the fresh state (below)
+        }  // else missing (or being claimed / failed): blk stays -1, the frames run from the fresh
+           // state (below) and the end of the item claims the block or waits for the claimer
     }
     float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
@@ -842,7 +847,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }
 #pragma unroll
         for (int h = 0; h < kH; ++h) loaded[h] |= need[h];
-        if (HASH) {
+        if constexpr (HASH) {
 #pragma unroll
             for (int k = 0; k < NZ; ++k) touched[k] |= __ballot(okv[k]);
         }
