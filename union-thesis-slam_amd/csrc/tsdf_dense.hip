@@ -156,11 +156,11 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
         const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0) | (dk == TSDF_DEPTH_U16_MM ? 0 : 4);
+        const FusedArgs args{B.vol, bi, bc, bp, B.pool, B.stats, sg};
         switch (sel) {
 #define TSDF_LAUNCH(S, OW_, NZ_, DK_)                                                                   \
     case S:                                                                                             \
-        hipLaunchKernelGGL((k_fused<OW_, NZ_, DK_>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, B.vol, \
-                           bi, bc, bp, B.pool, B.stats, sg);                                            \
+        hipLaunchKernelGGL((k_fused<OW_, NZ_, DK_>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, args); \
         break;
             TSDF_LAUNCH(0, false, 8, 0)
             TSDF_LAUNCH(1, true, 8, 0)

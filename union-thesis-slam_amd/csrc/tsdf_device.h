@@ -1530,6 +1530,19 @@ struct Stage {
     int* res_c;
 };
 
+// A pointer the compiler cannot see through: loads from it are neither merged with loads before
+// it nor speculated out of the conditional blocks that use them.  The fused launches read their
+// volume geometry, pool and (hash) table fields through such pointers to their own kernarg copy,
+// so those loads stay where the fields are used (scalar loads, scalar-cache hits) instead of being
+// hoisted to the kernel's entry and held in scalar registers across the item and frame loops,
+// where the frame constants and step masks need them: with them held, SGPRs spilled to VGPR lanes
+// (v_writelane / v_readlane, VALU instructions) and, in the hash launch, VGPRs to scratch.
+template <typename T>
+__device__ inline const __attribute__((address_space(4))) T* opaque(const __attribute__((address_space(4))) T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 #ifdef TSDF_WG_TIMES
 // Diagnostic builds only (tools/gpu/wg_times.py): per workgroup of the last full fused launch, its
 // start and end (s_memrealtime, 100 MHz) and role << 32 | the list items its waves took (role 0
@@ -1537,10 +1550,24 @@ struct Stage {
 constexpr int kWgTimes = 16384;
 __device__ unsigned long long g_wg_times[3][kWgTimes];
 #endif
+// The dense fused launch's arguments as one struct (the kernel addresses its kernarg copy).
+struct FusedArgs {
+    Vol v;
+    Batch bi, bc, bp;
+    Pool pool;
+    unsigned long long* stats;
+    Stage sg;
+};
+typedef const __attribute__((address_space(4))) FusedArgs* FusedArgsP;
+
 template <bool OW1, int NZ, int DK = 0>
-__global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_DENSE_WAVES))) void k_fused(Vol v, Batch bi, Batch bc, Batch bp,
-                                                                     Pool pool, unsigned long long* stats,
-                                                                     Stage sg) {
+__global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_DENSE_WAVES))) void k_fused(FusedArgs a) {
+    const FusedArgsP A = (FusedArgsP)__builtin_amdgcn_kernarg_segment_ptr();
+    const Vol& v = *(const Vol*)opaque(&A->v);
+    const Pool& pool = *(const Pool*)opaque(&A->pool);
+    const Batch &bi = a.bi, &bc = a.bc, &bp = a.bp;
+    unsigned long long* const stats = a.stats;
+    const Stage& sg = a.sg;
     // integrate: RN(1/n) table; cull: per-brick frame masks; prep: two pyramid tiles
     __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
@@ -1616,9 +1643,28 @@ __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolRepo
 #ifndef TSDF_FUSED_HASH_WAVES
 #define TSDF_FUSED_HASH_WAVES 6
 #endif
+// The launch's arguments as one struct, so that the kernel can address its own copy in the
+// kernarg segment (fused_args).
+struct FusedHashArgs {
+    Vol v;
+    Batch bi, bc, bp;
+    Pool pool;
+    Table tab;
+    unsigned long long* stats;
+    Stage sg;
+};
+
 template <int DK = 0>
 __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TSDF_FUSED_HASH_WAVES))) void k_fused_hash(
-        Vol v, Batch bi, Batch bc, Batch bp, Pool pool, Table tab, unsigned long long* stats, Stage sg) {
+        FusedHashArgs a) {
+    typedef const __attribute__((address_space(4))) FusedHashArgs* ArgsP;
+    const ArgsP A = (ArgsP)__builtin_amdgcn_kernarg_segment_ptr();
+    const Table& tab = *(const Table*)opaque(&A->tab);
+    const Vol& v = *(const Vol*)opaque(&A->v);
+    const Pool& pool = *(const Pool*)opaque(&A->pool);
+    const Batch &bi = a.bi, &bc = a.bc, &bp = a.bp;
+    unsigned long long* const stats = a.stats;
+    const Stage& sg = a.sg;
     __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ int s_last;

@@ -944,12 +944,11 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         }
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
+        const FusedHashArgs args{B.vol, bi, bc, bp, B.pool, h->t, B.stats, sg};
         if (dk == TSDF_DEPTH_U16_MM)
-            hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, B.vol, bi, bc,
-                               bp, B.pool, h->t, B.stats, sg);
+            hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
         else
-            hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, B.vol, bi, bc,
-                               bp, B.pool, h->t, B.stats, sg);
+            hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
         TSDF_HIP(hipGetLastError());
         if (!has_i) continue;
         TSDF_TRY(B.prof.end(B.stream, e0));
