@@ -1223,6 +1223,24 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, Li
 #ifndef TSDF_PRIO_MIN  // ... for workgroups with at least this many list items (brick parts)
 #define TSDF_PRIO_MIN 64
 #endif
+// A pointer the compiler cannot see through: loads from it are neither merged with loads before
+// it nor speculated out of the conditional blocks that use them.  The fused launches read their
+// volume geometry, pool and (hash) table fields through such pointers to their own kernarg copy,
+// so those loads stay where the fields are used (scalar loads, scalar-cache hits) instead of being
+// hoisted to the kernel's entry and held in scalar registers across the item and frame loops,
+// where the frame constants and step masks need them: with them held, SGPRs spilled to VGPR lanes
+// (v_writelane / v_readlane, VALU instructions) and, in the hash launch, VGPRs to scratch.
+template <typename T>
+__device__ inline const __attribute__((address_space(4))) T* opaque(const __attribute__((address_space(4))) T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+typedef const __attribute__((address_space(4))) Vol* VolP;
+// The volume of an item: re-read per item through an opaque pointer (v must be the launch's kernarg
+// copy), so its fields are not hoisted out of the item loop and held across it.
+__device__ inline const Vol& item_vol(const Vol& v) { return *(const Vol*)opaque((VolP)&v); }
+
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
@@ -1248,7 +1266,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
     constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[e / parts], (e % parts) * NZ,
+            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[e / parts], (e % parts) * NZ,
                                                    s_stat, s_rcp, nupd);
         return;
     }
@@ -1256,15 +1274,14 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
     // first, so that the round-robin hands every wave a similar amount of work (the longest-job-
     // first order of list scheduling)
     const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
-    unsigned ncls[kMaxBatch];
     int total = 0;
 #pragma unroll
-    for (int c = 0; c < kMaxBatch; ++c) {
-        ncls[c] = min(coh_load(&count[c + 1]), nbk);
-        total += (int)ncls[c];
-    }
+    for (int c = 0; c < kMaxBatch; ++c) total += (int)min(coh_load(&count[c + 1]), nbk);
     int c = kMaxBatch - 1;
     unsigned k0 = 0;  // list ordinal where class c starts (classes visited in descending order)
+    // the length of class c only (one scalar live across the items; the next class's is read when
+    // the walk reaches it -- at most kMaxBatch - 1 times per wave)
+    unsigned nc = min(coh_load(&count[c + 1]), nbk);
     if (s_next) {
         // Items dealt round-robin to workgroups (still longest first) and taken dynamically by
         // the workgroup's waves from an LDS counter: a wave that
@@ -1302,9 +1319,13 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             // share their depth / colour gathers in the CU's cache
             const long long k = (long long)wg + (long long)(j / parts) * n_wg;  // increasing for this wave
             if (k >= (long long)total) break;
-            while (c > 0 && (unsigned)k - k0 >= ncls[c]) k0 += ncls[c--];
+            while (c > 0 && (unsigned)k - k0 >= nc) {
+                k0 += nc;
+                --c;
+                nc = min(coh_load(&count[c + 1]), nbk);
+            }
             // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
+            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
                                                    (int)(j % parts) * NZ, s_stat, s_rcp, nupd, res);
         }
         if (use_prio) __builtin_amdgcn_s_setprio(0);
@@ -1312,8 +1333,12 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
     }
     for (int e = wave; e < total * parts; e += n_waves) {
         const unsigned k = (unsigned)(e / parts);
-        while (c > 0 && k - k0 >= ncls[c]) k0 += ncls[c--];
-        integrate_brick<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
+        while (c > 0 && k - k0 >= nc) {
+            k0 += nc;
+            --c;
+            nc = min(coh_load(&count[c + 1]), nbk);
+        }
+        integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
                                                (e % parts) * NZ, s_stat, s_rcp, nupd, res);
     }
 }
@@ -1333,6 +1358,8 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ = 8>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_WAVES))) void k_integrate(Vol v, Batch bt, Pool pool, Table tab,
                                                   unsigned long long* stats, const ListEntry* list,
                                                   unsigned int* count, int n_list) {
+    (void)v;  // read through its kernarg copy (the first parameter: offset 0), see item_vol
+    const Vol& vk = *(const Vol*)opaque((VolP)__builtin_amdgcn_kernarg_segment_ptr());
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ double s_rcp[OW1 ? kRcpTab : 1];  // RN(1/n): weights are small integers when ow == 1
     __shared__ unsigned s_next;                  // the workgroup's next list item (integrate_list)
@@ -1340,9 +1367,9 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(TSDF_HASH_W
     if (tid < kNStat) s_stat[tid] = 0;
     if (tid == 0) s_next = 0;
     if (OW1)  // 32 KB table copied with 16-byte loads (computing it cost 16 f64 divisions per thread)
-        for (int i = tid; i < kRcpTab / 2; i += kWG) ((double2*)s_rcp)[i] = ((const double2*)v.rcp)[i];
+        for (int i = tid; i < kRcpTab / 2; i += kWG) ((double2*)s_rcp)[i] = ((const double2*)vk.rcp)[i];
     __syncthreads();
-    integrate_list<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list, count, n_list,
+    integrate_list<HASH, DK, CK, OW1, NZ>(vk, bt, pool, tab, list, count, n_list,
                                           blockIdx.x * (kWG / 64) + (tid >> 6), gridDim.x * (kWG / 64),
                                           s_stat, OW1 ? s_rcp : nullptr, &s_next, blockIdx.x, gridDim.x);
     __syncthreads();
@@ -1529,19 +1556,6 @@ struct Stage {
     int* res_i;              // hash: per-brick claim words of batch k (integrate) and k+1 (cull)
     int* res_c;
 };
-
-// A pointer the compiler cannot see through: loads from it are neither merged with loads before
-// it nor speculated out of the conditional blocks that use them.  The fused launches read their
-// volume geometry, pool and (hash) table fields through such pointers to their own kernarg copy,
-// so those loads stay where the fields are used (scalar loads, scalar-cache hits) instead of being
-// hoisted to the kernel's entry and held in scalar registers across the item and frame loops,
-// where the frame constants and step masks need them: with them held, SGPRs spilled to VGPR lanes
-// (v_writelane / v_readlane, VALU instructions) and, in the hash launch, VGPRs to scratch.
-template <typename T>
-__device__ inline const __attribute__((address_space(4))) T* opaque(const __attribute__((address_space(4))) T* p) {
-    asm volatile("" : "+s"(p));
-    return p;
-}
 
 #ifdef TSDF_WG_TIMES
 // Diagnostic builds only (tools/gpu/wg_times.py): per workgroup of the last full fused launch, its
