@@ -263,20 +263,16 @@ def test_trim_hands_pool_memory_back_and_growth_resumes(monkeypatch):
     assert h.stats()["bricks_skipped"] == 0 or h.info()["pool_capacity"] > after["pool_capacity"]
 
 
-@pytest.mark.parametrize("recent_only", [False, True])
-def test_async_hash_growth_survives_a_turn_into_unseen_space(monkeypatch, recent_only):
+def test_async_hash_growth_survives_a_turn_into_unseen_space():
     """Advisor r03: asynchronous pool growth must not lag a growth spike.  A steady stretch (the
     same eight frames re-integrated with poses moved a few millimetres per batch: a few new blocks
-    per batch, so the recent growth is small), then the camera jumps to a far part of the
+    per batch, so the recent growth is small), then the camera jumps to the far side of the
     trajectory (thousands of new blocks per batch).  The room kept for the launches in flight
-    covers two of the cull's brick lists, so nothing is skipped and the result equals the dense
-    grid; round 3's rule (three recent growths only, the TSDF_HASH_ROOM_RECENT_ONLY hook) does
-    overflow here -- reported as TSDF_E_CAPACITY -- which is what makes this a test of the spike."""
-    from tsdf_amd import _ffi, grid_fusion, hash_fusion
-    if recent_only:
-        monkeypatch.setenv("TSDF_HASH_ROOM_RECENT_ONLY", "1")
+    covers two of the cull's brick lists besides the recent growth, so nothing is skipped (a skip
+    raises TSDF_E_CAPACITY at the sync) and the result equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
     d0, c0, p0 = _synth(8, start=100)
-    d1, c1, p1 = _synth(24, start=560)
+    d1, c1, p1 = _synth(24, start=600)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     steady = []
     for k in range(1, 7):  # six batches, each shifted 3 mm further along x
@@ -289,15 +285,14 @@ def test_async_hash_growth_survives_a_turn_into_unseen_space(monkeypatch, recent
     h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 16, max_blocks=1 << 12)
     h.integrate_batch(d[:8], c[:8], K, Tinv[:8])  # synchronous start (its overflows re-run exactly)
     skipped0 = h.stats()["bricks_skipped"]
-    if recent_only:
-        with pytest.raises(_ffi.TSDFError) as ei:
-            h.integrate_batch(d[8:], c[8:], K, Tinv[8:], sync=False)
-            h.sync()
-        assert ei.value.code == _ffi.E_CAPACITY
-        return
-    h.integrate_batch(d[8:], c[8:], K, Tinv[8:], sync=False)
+    used0 = h.info()["used"]
+    h.integrate_batch(d[8:64], c[8:64], K, Tinv[8:64], sync=False)
+    h.sync()
+    used1 = h.info()["used"]
+    h.integrate_batch(d[64:], c[64:], K, Tinv[64:], sync=False)
     h.sync()  # raises TSDF_E_CAPACITY if a launch in flight ran out of pool
     assert h.stats()["bricks_skipped"] == skipped0
+    assert used1 - used0 < (h.info()["used"] - used1) / 4  # a steady stretch, then a spike
     g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
     g.integrate_batch(d, c, K, Tinv)
     for a, b in zip(g.get_state(), h.get_state()):

@@ -9,9 +9,11 @@ bench line printed under the profiler):
   profiles/pmc_integrate_<tag>.json    HBM traffic per timed integrate launch (FETCH_SIZE/WRITE_SIZE)
   profiles/pmc_sq_<tag>.json           SQ issue counters per timed integrate launch
 
-The timed launches: bench.py's warm-up call of W batches issues W + 2 pipelined launches of
-k_fused<true, 4, 0>, the timed call 2 + K of them, the last K of which integrate; so they are the
-launches W + 4 .. W + 3 + K of that kernel in dispatch order (the ingest leg's launches follow).
+The timed launches: every bench.py call of n batches issues n + 2 pipelined launches of
+k_fused<true, 4, 0> (the cold window, the clock warm-up, the W warm-up steps, then the timed call,
+whose first two launches fill the pipeline); the bench line records the dispatch-order index of
+the first timed integrate launch (roofline.first_timed_launch_index), and the K launches from it
+are the timed ones.
 
 FETCH_SIZE/WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
 coalesced read (MI355X_MICROARCH.md, HBM section); the integrate kernel's HBM reads are its
@@ -35,20 +37,21 @@ def bench_line(path):
         return json.loads([l for l in f if l.startswith("{")][-1])
 
 
-def timed(rows_by_dispatch):
-    """rows_by_dispatch: [(dispatch_id, row)] of KERNEL in dispatch order -> the K timed launches."""
+def timed(rows_by_dispatch, first):
+    """rows_by_dispatch: [(dispatch_id, row)] of KERNEL -> the K timed launches, from the index the
+    bench line records (roofline.first_timed_launch_index)."""
     rows = sorted(rows_by_dispatch, key=lambda r: r[0])
-    return rows[W + 4:W + 4 + K]
+    return rows[first:first + K]
 
 
-def pmc_timed(path, counter):
+def pmc_timed(path, counter, first):
     per = {}
     for row in csv.DictReader(open(path)):
         if row["Counter_Name"] != counter or KERNEL not in row["Kernel_Name"]:
             continue
         d = int(row["Dispatch_Id"])
         per[d] = per.get(d, 0.0) + float(row["Counter_Value"])  # (summed over dimensions / XCDs)
-    t = timed(list(per.items()))
+    t = timed(list(per.items()), first)
     return [v for _, v in t]
 
 
@@ -64,7 +67,7 @@ def main(tag):
     # the timed launches' trace rows
     trace = [r for r in csv.DictReader(open(os.path.join(src, "kernel_trace_tsdf.csv")))
              if KERNEL in r["Kernel_Name"]]
-    t = timed([(int(r["Dispatch_Id"]), r) for r in trace])
+    t = timed([(int(r["Dispatch_Id"]), r) for r in trace], line["roofline"]["first_timed_launch_index"])
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for _, r in t]
     with open(os.path.join(dst, f"{tag}_timed_launches.csv"), "w") as f:
         f.write(f"# {KERNEL}: the {K} timed integrate launches of bench.py --gpus 1 --steps {K} --warmup {W} "
@@ -73,9 +76,10 @@ def main(tag):
         f.write("dispatch_id,start_ns,end_ns,duration_us\n")
         for (d, r), us in zip(t, durs):
             f.write(f"{d},{r['Start_Timestamp']},{r['End_Timestamp']},{us:.2f}\n")
-    fetch = pmc_timed(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
-    write = pmc_timed(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
     pl = bench_line(os.path.join(src, "pmc_FETCH_SIZE.json"))
+    pw = bench_line(os.path.join(src, "pmc_WRITE_SIZE.json"))
+    fetch = pmc_timed(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", pl["roofline"]["first_timed_launch_index"])
+    write = pmc_timed(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", pw["roofline"]["first_timed_launch_index"])
     sys.path.insert(0, REPO)
     import bench
     fk = statistics.median(fetch) * 1024.0
@@ -98,8 +102,9 @@ def sq(tag):
     src = os.path.join(REPO, "gpurun_out", "pmc_sq")
     names = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
              "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
-    med = {c: statistics.median(pmc_timed(os.path.join(src, "pmc_sq.csv"), c)) for c in names}
     pl = bench_line(os.path.join(src, "bench.json"))
+    first = pl["roofline"]["first_timed_launch_index"]
+    med = {c: statistics.median(pmc_timed(os.path.join(src, "pmc_sq.csv"), c, first)) for c in names}
     sys.path.insert(0, REPO)
     import bench
     out = {"kernel": KERNEL, "build_id": pl.get("build_id"), "median_per_launch": med,

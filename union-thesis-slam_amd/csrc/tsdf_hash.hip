@@ -177,9 +177,6 @@ struct tsdf_hash {
     // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
     // 156-161); TSDF_HASH_MAX_LOAD overrides it for the load-factor sweep (tools/hash_sweep.py)
     double max_load = 0.75;
-    // test hook (TSDF_HASH_ROOM_RECENT_ONLY=1): round 3's asynchronous room, three recent growths
-    // only -- the spike test shows that it overflows where the cull-list bound does not
-    bool room_recent_only = false;
     // block pool on reserved address ranges (tsdf, weight, colour, entry words, free list)
     bool vmm = false;
     VArray va[5];
@@ -808,7 +805,7 @@ int async_room(tsdf_hash* h, long long s) {
     h->note_live(used);
     // (the copy path keeps the pool's 1/12 as a floor of the estimate too, and doubles)
     const long long step = h->vmm ? h->recent_growth() : std::max<long long>(h->recent_growth(), h->t.max_blocks / 12);
-    const long long need = used + (h->room_recent_only ? 3 * step : std::max<long long>(3 * step, 2 * r.listed + step));
+    const long long need = used + std::max<long long>(3 * step, 2 * r.listed + step);
     if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, pool_target(h, need + step)));
     while ((double)(used + 3 * h->recent_growth() + h->tomb_est) >= h->max_load * (double)h->map_size)
         TSDF_TRY(grow_table(h));
@@ -1231,7 +1228,6 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
     }
     if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;  // 0: in-line kernels
     if (const char* e = getenv("TSDF_HASH_VMM_FAIL")) h->vmm_fail_at = atoi(e);  // (after the initial mapping)
-    if (const char* e = getenv("TSDF_HASH_ROOM_RECENT_ONLY")) h->room_recent_only = atoi(e) != 0;
     if (const char* e = getenv("TSDF_HASH_MAX_LOAD")) {
         const double ml = atof(e);
         if (ml > 0.0 && ml < 1.0) h->max_load = ml;
