@@ -264,37 +264,39 @@ def test_trim_hands_pool_memory_back_and_growth_resumes(monkeypatch):
 
 
 def test_async_hash_growth_survives_a_turn_into_unseen_space():
-    """Advisor r03: asynchronous pool growth must not lag a growth spike.  A steady stretch (the
-    same eight frames re-integrated with poses moved a few millimetres per batch: a few new blocks
-    per batch, so the recent growth is small), then the camera jumps to the far side of the
-    trajectory (thousands of new blocks per batch).  The room kept for the launches in flight
-    covers two of the cull's brick lists besides the recent growth, so nothing is skipped (a skip
-    raises TSDF_E_CAPACITY at the sync) and the result equals the dense grid."""
-    from tsdf_amd import grid_fusion, hash_fusion
-    d0, c0, p0 = _synth(8, start=100)
-    d1, c1, p1 = _synth(24, start=600)
+    """Advisor r03: asynchronous pool growth must not lag a growth spike.  A camera on the scene's
+    sphere-free ring looks along the ring one way (eight frames, integrated once synchronously
+    and then five more times asynchronously: no new blocks, so the recent growth is zero), then
+    turns to look the other way (as far, as wide, all of it unseen: the whole list is new blocks).
+    The room kept for the launches in flight covers two of the cull's brick lists besides the
+    recent growth, so nothing is skipped (a skip raises TSDF_E_CAPACITY at the sync) and the
+    result equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion, scene
+    c, R = 5.12, 0.34 * 10.24
+    eye = np.array([c + R, c, c])
+    poses = []
+    for k in range(16):  # 8 looking +y, then 8 looking -y (small target jitter within each)
+        sgn = 1.0 if k < 8 else -1.0
+        poses.append(scene.look_at(eye, eye + np.array([0.02 * (k % 4), sgn * 5.0, 0.01 * (k % 3)])))
+    poses = np.stack(poses)
+    dd, cc = scene.render(poses, scene.make_spheres(0), seed=0, start=900)
+    dd, cc = np.ascontiguousarray(dd.numpy()), np.ascontiguousarray(cc.numpy())
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
-    steady = []
-    for k in range(1, 7):  # six batches, each shifted 3 mm further along x
-        pk = p0.copy()
-        pk[:, 0, 3] += 0.003 * k
-        steady.append(pk)
-    d = np.concatenate([d0] * 7 + [d1])
-    c = np.concatenate([c0] * 7 + [c1])
-    Tinv = np.linalg.inv(np.concatenate([p0] + steady + [p1]))
+    idx = list(range(8)) * 6 + list(range(8, 16)) * 2  # steady x 6 (first one synchronous), turn x 2
+    d, col, Tinv = dd[idx], cc[idx], np.linalg.inv(poses[idx])
     h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 16, max_blocks=1 << 12)
-    h.integrate_batch(d[:8], c[:8], K, Tinv[:8])  # synchronous start (its overflows re-run exactly)
+    h.integrate_batch(d[:8], col[:8], K, Tinv[:8])  # synchronous start (its overflows re-run exactly)
     skipped0 = h.stats()["bricks_skipped"]
     used0 = h.info()["used"]
-    h.integrate_batch(d[8:64], c[8:64], K, Tinv[8:64], sync=False)
+    h.integrate_batch(d[8:48], col[8:48], K, Tinv[8:48], sync=False)
     h.sync()
     used1 = h.info()["used"]
-    h.integrate_batch(d[64:], c[64:], K, Tinv[64:], sync=False)
+    h.integrate_batch(d[48:], col[48:], K, Tinv[48:], sync=False)
     h.sync()  # raises TSDF_E_CAPACITY if a launch in flight ran out of pool
     assert h.stats()["bricks_skipped"] == skipped0
-    assert used1 - used0 < (h.info()["used"] - used1) / 4  # a steady stretch, then a spike
+    assert used1 == used0 and h.info()["used"] - used1 > used0 / 2  # steady, then a spike
     g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
-    g.integrate_batch(d, c, K, Tinv)
+    g.integrate_batch(d, col, K, Tinv)
     for a, b in zip(g.get_state(), h.get_state()):
         assert np.array_equal(a, b)
 

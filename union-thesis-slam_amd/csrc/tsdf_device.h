@@ -1076,16 +1076,20 @@ __device__ inline int cull_lookup(const Vol& v, const Table& t, unsigned e, unsi
     const int nb12 = v.nb[1] * v.nb[2];
     const int bx = (int)e / nb12, r = (int)e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
     const unsigned long long key = pack_key(bx, by, bz);
-    const long long mask = t.capacity - 1;
-    long long s = ref_hash<true>(bx, by, bz, t.capacity, t.int_bits);
-    for (long long n = 0; n < t.capacity; ++n) {
-        const unsigned long long k = coh_load(&t.keys[s]);
+    // the table's fields once, into registers (t may be read through an opaque pointer: opaque)
+    unsigned long long* const keys = t.keys;
+    int* const vals = t.vals;
+    const long long cap = t.capacity, max_blocks = t.max_blocks;
+    const long long mask = cap - 1;
+    long long s = ref_hash<true>(bx, by, bz, cap, t.int_bits);
+    for (long long n = 0; n < cap; ++n) {
+        const unsigned long long k = coh_load(&keys[s]);
         if (k == key) {
-            const int blk = coh_load(&t.vals[s]);
+            const int blk = coh_load(&vals[s]);
             atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
             atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
             atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
-            return (blk >= 0 && blk < t.max_blocks) ? blk : kResFree;
+            return (blk >= 0 && blk < max_blocks) ? blk : kResFree;
         }
         if (k == kEmpty) break;
         s = (s + 1) & mask;
@@ -1684,6 +1688,10 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
     __shared__ int s_last;
     __shared__ unsigned s_next;
     const int tid = threadIdx.x, b = blockIdx.x;
+#ifdef TSDF_WG_TIMES
+    const bool rec = sg.gi > 0 && sg.gc > 0 && (int)gridDim.x > sg.gi + sg.gc && b < kWgTimes;
+    if (tid == 0 && rec) g_wg_times[0][b] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
         if (tid == 0) s_next = 0;
@@ -1715,6 +1723,14 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         float(*sa)[33] = (float(*)[33])s_buf;
         prep_vec_tile<DK>(bp, sg.count_p, r % sg.ptx, r / sg.ptx, f, sa, sa + 32);
     }
+#ifdef TSDF_WG_TIMES
+    __syncthreads();
+    if (tid == 0 && rec) {
+        g_wg_times[1][b] = __builtin_amdgcn_s_memrealtime();
+        g_wg_times[2][b] = ((unsigned long long)(b < sg.gi ? 0 : b < sg.gi + sg.gc ? 1 : 2) << 32) |
+                           (b < sg.gi ? s_next : 0u);
+    }
+#endif
 }
 
 }  // namespace tsdf

@@ -166,7 +166,7 @@ struct tsdf_hash {
     int n_delta = 0;
     void note_live(long long used) {  // a new live-block count: remember its growth (from 0 at first)
         const long long prev = rb_used < 0 ? 0 : rb_used;
-        if (used > prev) deltas[n_delta++ & 3] = used - prev;
+        if (used != prev || rb_used < 0) deltas[n_delta++ & 3] = used > prev ? used - prev : 0;
         rb_used = used;
     }
     long long recent_growth() const {  // the largest of the recent growths (at least 256 blocks)
@@ -1645,3 +1645,12 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 }
 
 }  // extern "C"
+
+#ifdef TSDF_WG_TIMES
+// (diagnostic builds) the last fused hash launch's per-workgroup start / end / role|items
+extern "C" int tsdf_diag_wg_times_hash(unsigned long long* out) {
+    TSDF_HIP(hipDeviceSynchronize());
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 3 * kWgTimes));
+    return TSDF_OK;
+}
+#endif
