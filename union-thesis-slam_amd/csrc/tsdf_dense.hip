@@ -59,10 +59,11 @@ int dense_run_inline(tsdf_dense* h, int n_frames, const void* depth, int dk, con
     const unsigned grid = h->nz == 4 ? 2 * B.grid_for((const void*)k_integrate<false, 0, 0, true, 4>)
                                      : B.grid_for((const void*)k_integrate<false, 0, 0, true, 8>);
     B.use_set(0);
-    for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
+    const int nbat = B.batch;
+    for (int f0 = 0; f0 < n_frames; f0 += nbat) {
         Batch bt;
-        const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
-        const int slot = (f0 / kMaxBatch) % kSlots;
+        const int n = n_frames - f0 < nbat ? n_frames - f0 : nbat;
+        const int slot = (f0 / nbat) % kSlots;
         TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, ow, 1.0, flags, f0, n, slot));
         TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, B.stream));
         hipLaunchKernelGGL((k_cull<false>), dim3(cull_grid), dim3(kCullWG), 0, B.stream, B.vol, bt, no_table,
@@ -114,7 +115,8 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
                     int W, const double* K, const double* Tinv, const double* ow, int flags) {
     Base& B = h->b;
     TSDF_TRY(B.use_sets(kSets));
-    const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
+    const int nbat = B.batch;
+    const int nb = (n_frames + nbat - 1) / nbat;
     const int gi_occ = h->nz == 4 ? (int)B.grid_for((const void*)k_fused<true, 4>, kFusedWG)
                                   : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
     const int gi_full = h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ;
@@ -123,8 +125,8 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;  // batch prepped by this launch
         if (jp < nb) {
-            const int f0 = jp * kMaxBatch;
-            const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+            const int f0 = jp * nbat;
+            const int n = n_frames - f0 < nbat ? n_frames - f0 : nbat;
             B.use_set(jp % kSets);
             TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, dk, color, TSDF_COLOR_RGB8, H, W,
                                      K, Tinv, ow, 1.0, flags, f0, n, jp % kSlots));
@@ -285,6 +287,7 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
             h->b.vol.sb[0] = 0;
             h->b.vol.sb[1] = h->b.vol.sb[2] = 3;
         }
+        h->b.set_batch(xstride > kBrickEdge ? kMaxBatch : kFullBatch);
         const int64_t last = h->b.vol.nb[0] - 1;
         const int64_t gx_max = (int64_t)h->b.vol.off[0] + (last >> 1) * 2 * (int64_t)xstride + (last & 1) * (int64_t)xodd + kBrickEdge;
         if (gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
@@ -385,7 +388,7 @@ int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, con
         if (flags & TSDF_DEVICE_PTRS) return set_error(TSDF_E_ARG, "TSDF_DEFER takes host frames only");
         if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(dense_flush(h));
         TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, obs_weight));
-        if (B.dfr.n == kMaxBatch) TSDF_TRY(dense_flush(h));
+        if (B.dfr.n == B.batch) TSDF_TRY(dense_flush(h));
         return TSDF_OK;
     }
     TSDF_TRY(dense_flush(h));

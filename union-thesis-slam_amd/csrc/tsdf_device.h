@@ -92,6 +92,13 @@ struct PyrGeo {
 #endif
 constexpr int kMaxBatch = TSDF_MAX_BATCH;
 static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
+// Frames per launch of a whole (unsharded) volume; shards of a multi-GPU volume take kMaxBatch
+// (Base::set_batch): a shard's launch is short, and its fixed costs -- dispatch, the end of the
+// kernel, the cull / prep tail -- weigh more per frame.
+#ifndef TSDF_FULL_BATCH
+#define TSDF_FULL_BATCH TSDF_MAX_BATCH
+#endif
+constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxBatch;
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
 constexpr int kCountWords = 32, kDoneWord = 24;

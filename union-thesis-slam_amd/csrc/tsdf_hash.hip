@@ -878,7 +878,8 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
                    const double* K, const double* Tinv, int flags) {
     Base& B = h->b;
     const bool sync = !(flags & TSDF_ASYNC);
-    const bool later = sync && (flags & kCheckLater) && n_frames <= kMaxBatch;
+    const int nbat = B.batch;
+    const bool later = sync && (flags & kCheckLater) && n_frames <= nbat;
     // a pending batch's exact re-run reads its buffer set and staging slot: settle it first if this
     // call reallocates per-batch buffers (first fused call, another image size)
     if (h->pend.on && !(B.n_sets >= kSets && B.pyr_H == H && B.pyr_W == W && B.stage_fits(dk, TSDF_COLOR_RGB8, H, W)))
@@ -886,7 +887,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     TSDF_TRY(B.use_sets(kSets));
     const int rot = h->set_rot;
     const auto set_of = [rot](int j) { return (j + rot) % kSets; };
-    const int nb = (n_frames + kMaxBatch - 1) / kMaxBatch;
+    const int nb = (n_frames + nbat - 1) / nbat;
     if (!h->d_res) {  // each word is written by the cull that lists its brick before an integrate reads it
         if (h->t.max_blocks >= kResNew || B.n_bricks >= (1ll << 31) / kSets)
             return set_error(TSDF_E_ARG, "volume too large for the claim words");
@@ -901,8 +902,8 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;
         if (jp < nb) {
-            const int f0 = jp * kMaxBatch;
-            const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
+            const int f0 = jp * nbat;
+            const int n = n_frames - f0 < nbat ? n_frames - f0 : nbat;
             B.use_set(set_of(jp));
             // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
             TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, dk, color, TSDF_COLOR_RGB8, H, W,
@@ -977,15 +978,16 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
     TSDF_HIP(hipSetDevice(B.device));
     const unsigned cull_grid = h->t.owned ? (unsigned)std::max(1, (h->t.n_owned + 63) / 64) : B.cull_grid();
     const bool sync = !(flags & TSDF_ASYNC);
-    if (!sync && h->rb_used < 0 && n_frames > kMaxBatch && B.prestaged < 0) {
+    if (!sync && h->rb_used < 0 && n_frames > B.batch && B.prestaged < 0) {
         // A fresh table's first asynchronous call: its first batch runs synchronously (the pool
         // grows exactly and skipped bricks re-run), so the growth of the batches in flight is
         // known before any launch depends on a lagging report.
-        TSDF_TRY(hash_run(h, kMaxBatch, depth, dk, color, ck, H, W, K, Tinv, flags & ~TSDF_ASYNC));
-        depth = (const char*)depth + frame_bytes_depth(dk, H, W) * kMaxBatch;
-        color = (const char*)color + frame_bytes_color(ck, H, W) * kMaxBatch;
-        Tinv += 16 * kMaxBatch;
-        n_frames -= kMaxBatch;
+        const int nbat = B.batch;
+        TSDF_TRY(hash_run(h, nbat, depth, dk, color, ck, H, W, K, Tinv, flags & ~TSDF_ASYNC));
+        depth = (const char*)depth + frame_bytes_depth(dk, H, W) * nbat;
+        color = (const char*)color + frame_bytes_color(ck, H, W) * nbat;
+        Tinv += 16 * nbat;
+        n_frames -= nbat;
     }
     if (sync && h->async_pending) TSDF_TRY(take_overflow(h));  // before any replay of this call
     if (!sync) h->async_pending = true;
@@ -1008,10 +1010,11 @@ int hash_run(tsdf_hash* h, int n_frames, const void* depth, int dk, const void* 
         return TSDF_OK;
     }
     B.use_set(0);
-    for (int f0 = 0; f0 < n_frames; f0 += kMaxBatch) {
+    const int nbat = B.batch;
+    for (int f0 = 0; f0 < n_frames; f0 += nbat) {
         Batch bt;
-        const int n = n_frames - f0 < kMaxBatch ? n_frames - f0 : kMaxBatch;
-        const int slot = (f0 / kMaxBatch) % kSlots;
+        const int n = n_frames - f0 < nbat ? n_frames - f0 : nbat;
+        const int slot = (f0 / nbat) % kSlots;
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
         TSDF_TRY(B.prepare_batch(&bt, depth, dk, color, ck, H, W, K, Tinv, nullptr, 1.0, flags, f0, n, slot));
         TSDF_TRY(B.launch_prep(bt, dk, ck, W, H, B.stream));
@@ -1160,6 +1163,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
     if (r == TSDF_OK) {
         h->b.vol.shard = shard;
         h->b.vol.n_shards = n_shards;
+        h->b.set_batch(n_shards > 1 ? kMaxBatch : kFullBatch);
         if (max_blocks <= 0) max_blocks = std::min<long long>(h->b.n_bricks, 1 << 16);
         max_blocks = std::max<long long>(std::min<long long>(max_blocks, h->b.n_bricks), 64);
         h->map_size = capacity;
@@ -1300,7 +1304,7 @@ int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const
         if (h->pend.on && !B.stage_fits(depth_kind, color_kind, height, width)) TSDF_TRY(hash_settle(h));
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1
         TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0));
-        if (B.dfr.n == kMaxBatch) TSDF_TRY(hash_flush(h, false));
+        if (B.dfr.n == B.batch) TSDF_TRY(hash_flush(h, false));
         return TSDF_OK;
     }
     TSDF_TRY(hash_flush(h));

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <utility>
@@ -68,6 +69,13 @@ struct Base {
     Vol vol{};
     Pool pool{};
     long long n_bricks = 0;
+    // frames per launch (<= kMaxBatch, the kernels' Batch capacity): kMaxBatch for shards of a
+    // multi-GPU volume, kFullBatch for whole volumes (set_batch; TSDF_BATCH overrides)
+    int batch = kMaxBatch;
+    void set_batch(int want) {
+        if (const char* e = getenv("TSDF_BATCH")) want = atoi(e);
+        batch = want < 1 ? 1 : want > kMaxBatch ? kMaxBatch : want;
+    }
     // Per-batch buffers of the CURRENT buffer set (use_set).
     float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
     unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
