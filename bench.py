@@ -7,8 +7,8 @@
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-A step is one batch of 8 frames (the unit the kernels fuse: one three-stage k_fused launch
-integrates 8 frames with the brick state held in registers).  The F synthetic frames
+A step is one launch's batch of frames (the unit the kernels fuse: one three-stage k_fused launch
+integrates 16 frames with the brick state held in registers; TSDFVolume.frames_per_launch).  The F synthetic frames
 (tsdf_amd.scene: ray-cast room with spheres seen from the BENCH_RING trajectory, mean V_f 11.7 %
 of the volume; u16 millimetre depth, RGB) are generated directly in HBM before timing; W warmup
 steps, then K timed steps issued asynchronously, bracketed by barrier + synchronize; the max over
@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOM = 10.24
 VOXEL = 0.02
 PIX = 640 * 480
-BATCH = 8  # frames per step (kMaxBatch)
+BATCH = 16  # frames per step = frames per launch (set from the library: TSDFVolume.frames_per_launch)
 WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) into 512^3 @ 2 cm dense grid"
 # the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), quoted only when
 # their workload AND the build id of the library they measured match the loaded library
@@ -347,6 +347,8 @@ def main():
     bnds = np.array([[0.0, ROOM]] * 3)
     with contextlib.redirect_stdout(sys.stderr):  # the reference-style ctor prints; keep stdout JSON-only
         vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=gpu, shard=(rank, n))
+    global BATCH
+    BATCH = vol.frames_per_launch()  # a step = one launch's temporal batch (16 frames)
     W, Ks = args.warmup, args.steps
     Wf, Kf = W * BATCH, Ks * BATCH
     cold = None

@@ -48,7 +48,8 @@ extern "C" {
                                       of the demos (grid_demo1.py:82: depth_im[depth_im == 65.535] = 0) */
 #define TSDF_DEFER 8        /* tsdf_*_integrate (host frames only): copy the frame into a pinned
                                staging batch and return; the batch runs (asynchronously, as one
-                               temporally batched launch) once it holds 8 frames or at the next
+                               temporally batched launch) once it holds a launch's frames
+                               (tsdf_dense_frames_per_launch: 16) or at the next
                                other call on the handle -- the reference's one-integrate()-per-
                                frame loop (grid_demo1.py:76-87) at batched speed, same results.
                                Hash: a full table / pool found after a deferred batch is grown
@@ -138,6 +139,9 @@ int tsdf_dense_integrate_batch(tsdf_dense_t* h, int n_frames, const void* depth,
 int tsdf_dense_get(tsdf_dense_t* h, float* tsdf, float* weight, float* color);
 int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf, const float* weight, const float* color);
 int tsdf_dense_sync(tsdf_dense_t* h);
+/* Frames one launch integrates (the temporal batch: 16 in this build, 8 with -DTSDF_MAX_BATCH=8;
+ * TSDF_BATCH overrides per process); calls of n frames run ceil(n / batch) + 2 pipelined launches. */
+int tsdf_dense_frames_per_launch(tsdf_dense_t* h, int* n);
 /* Mesh of the shard's tsdf at level 0 (get_mesh / get_point_cloud, grid_fusion.py:322-360; the
  * reference runs skimage's marching_cubes_lewiner on the host).  extract runs marching cubes on
  * the device and keeps the result in the handle; get_mesh copies it out: verts n_verts x 3 f32

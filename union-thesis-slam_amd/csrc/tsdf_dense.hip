@@ -422,6 +422,12 @@ int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf_, const float* weight_, co
     return TSDF_OK;
 }
 
+int tsdf_dense_frames_per_launch(tsdf_dense_t* h, int* n) {
+    if (!h || !n) return set_error(TSDF_E_ARG, "null pointer");
+    *n = h->b.batch;
+    return TSDF_OK;
+}
+
 int tsdf_dense_sync(tsdf_dense_t* h) {
     if (!h) return set_error(TSDF_E_ARG, "null handle");
     TSDF_HIP(hipSetDevice(h->b.device));

@@ -87,8 +87,10 @@ struct PyrGeo {
 // Up to kMaxBatch consecutive frames integrated by one launch (temporal batching: each voxel's
 // updates are still applied frame by frame, in order, so results are those of one-by-one
 // integration; the brick state is read and written once per batch instead of once per frame).
+// 16 frames per launch (round 4: +6 % dense and +19 % hash on one GPU, +7 % / +27 % on eighth
+// shards against 8, profiles/r04_e/); 8 remains a build option (-DTSDF_MAX_BATCH=8)
 #ifndef TSDF_MAX_BATCH
-#define TSDF_MAX_BATCH 8
+#define TSDF_MAX_BATCH 16
 #endif
 constexpr int kMaxBatch = TSDF_MAX_BATCH;
 static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
@@ -543,7 +545,7 @@ __device__ inline double readlane_f64(double x, int l) {
 // it only where a voxel needs it).  The per-step conditions stay booleans (lane
 // masks in SGPR pairs): their combinations and wave ballots are scalar instructions, not VALU.
 template <int DK, int CK, int NZ>
-__device__ __forceinline__ void project_part(const Vol& v, const Frame& fr, double px, double py,
+__device__ __forceinline__ void project_part(double trunc, const Frame& fr, double px, double py,
                                              const double* pzs, double pz_l, int zoff, bool col_in, int nz,
                                              unsigned (&cpx)[NZ], double (&diff)[NZ], bool (&ok)[NZ]) {
     constexpr int kPz = NZ < 8 ? NZ : 1;
@@ -627,12 +629,14 @@ __device__ __forceinline__ void project_part(const Vol& v, const Frame& fr, doub
     for (int k = 0; k < NZ; ++k) {
         diff[k] = dep[k] - zc[k];
         const bool dpos = DK == 0 ? draw[k] != 0u : dep[k] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
-        ok[k] = cand[k] & dpos & (diff[k] >= -v.trunc);
+        ok[k] = cand[k] & dpos & (diff[k] >= -trunc);
     }
 }
 
 // np.minimum(1, (depth - z) / trunc) (grid_fusion.py:284-286; the quotient is never NaN)
-__device__ inline double dist_of(const Vol& v, double diff) { return fmin(div_rn(diff, v.trunc, v.rtrunc), 1.0); }
+__device__ inline double dist_of(double trunc, double rtrunc, double diff) {
+    return fmin(div_rn(diff, trunc, rtrunc), 1.0);
+}
 
 // Hash z-half waves (NZ = 4, the fused hash launch).  The two halves of a brick are waves 2m and
 // 2m+1 of one workgroup (integrate_list with an even wave count per workgroup) and meet in the
@@ -681,6 +685,15 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const int lane = lane_id();
     const int b = (int)(entry & 0xFFFFFFFFull);
     const unsigned fmask = (unsigned)(entry >> 32);
+    // the volume fields the frame loop reads, once per item (v is re-read per item through an
+    // opaque pointer, item_vol: its other fields are not held across the frame loop)
+    const double trunc = v.trunc, rtrunc = v.rtrunc;
+    const double* const rcp_hbm = v.rcp;
+    const bool canon = v.canon != 0;
+    [[maybe_unused]] int cur_pref = kResFree;
+    if constexpr (kHalfHash)  // (issued now, waited for where it is used; the bound check is below)
+        cur_pref = b < v.nb[0] * v.nb[1] * v.nb[2] ? __hip_atomic_load(res + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                                   : kResFree;
     const int nb12 = v.nb[1] * v.nb[2];
     if (b >= v.nb[0] * nb12) {  // never for a list k_cull wrote; guards the pool against bad input
         if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
@@ -711,7 +724,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     bool is_new = false;
     [[maybe_unused]] int* const rp = kHalfHash ? res + b : nullptr;
     if constexpr (kHalfHash) {
-        int cur = res_load(rp);  // the cull's lookup (or kResFree), written by the previous launch
+        // the cull's lookup (or kResFree), written by the previous launch: a relaxed read issued
+        // with the item's first instructions and used after its setup (a plain block needs no
+        // ordering); a negative value or a block this launch inserted (kResNew) is read again with
+        // acquire semantics
+        int cur = cur_pref;
+        if (cur < 0 || (cur & kResNew)) cur = res_load(rp);
         if (cur >= 0) {
         } else if (zoff == 0) {  // not found by the cull: the z-low wave looks again, for both halves
             long long slot = 0, probe = 0;
@@ -775,7 +793,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         unsigned cpx[NZ];
         double diff[NZ];
         bool okv[NZ];
-        project_part<DK, CK, NZ>(v, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
+        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
         bool need[kH];
 #pragma unroll
         for (int h = 0; h < kH; ++h) need[h] = okv[4 * h] | okv[4 * h + 1] | okv[4 * h + 2] | okv[4 * h + 3];
@@ -830,7 +848,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const float4 T = *(const float4*)(pool.tsdf + base + 4 * h);
                 const float4 C = *(const float4*)(pool.color + base + 4 * h);
                 ws[4 * h + 0] = W.x; ws[4 * h + 1] = W.y; ws[4 * h + 2] = W.z; ws[4 * h + 3] = W.w;
-                if (v.canon) {  // integers >= 0 and canonical colours by construction: a range test
+                if (canon) {  // integers >= 0 and canonical colours by construction: a range test
                     const float wm = fmaxf(fmaxf(W.x, W.y), fmaxf(W.z, W.w));
                     w_small = w_small && wm < (float)(kRcpTab - kMaxBatch - 1);
                     w_table = w_table && wm < (float)(kRcpBig - kMaxBatch - 1);
@@ -871,13 +889,13 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             // f32 expression of the scalar form, so the results are bit-identical to it.
             // RN(1/wn) from the LDS table, or from the HBM table past its limit through a buffer
             // load (a different instruction, so the two are never merged into a flat load)
-            const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)v.rcp, 0, kRcpBig * 8, kBufDword3);
+            const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)rcp_hbm, 0, kRcpBig * 8, kBufDword3);
             // Free space (wave-uniform): every updating voxel is at least trunc in front of the
             // surface (dist = min(1, diff / trunc) = 1 exactly) and still holds tsdf 1, so its new
             // tsdf is (w * 1 + 1) / (w + 1) = 1 exactly: the distance and tsdf quotients are skipped
             bool busy = false;
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) busy |= okv[k] & ((diff[k] < v.trunc) | (ts[k] != 1.0f));
+            for (int k = 0; k < NZ; ++k) busy |= okv[k] & ((diff[k] < trunc) | (ts[k] != 1.0f));
             const bool free_space = __ballot(busy) == 0;
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
@@ -904,7 +922,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const double num = (double)wt2[j] + dist_of(v, diff[k + j]);
+                        const double num = (double)wt2[j] + dist_of(trunc, rtrunc, diff[k + j]);
                         tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
                         r2[j] = (float)y[j];
                     }
@@ -935,10 +953,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             for (int k = 0; k < NZ; ++k) {
                 const float w_old = ws[k];
                 const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
-                const double dist = dist_of(v, diff[k]);
+                const double dist = dist_of(trunc, rtrunc, diff[k]);
                 const double num = (double)(w_old * ts[k]) + (OW1 ? dist : fr.ow * dist);
                 if (fast_t) tqv[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
-                else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, v.rcp[(int)wn]);
+                else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, rcp_hbm[(int)wn]);
                 else tqv[k] = (float)(num / (double)wn);
                 wnv[k] = wn;
                 // colour (grid_fusion.py:302-314): float32 throughout, round half to even
@@ -1311,7 +1329,10 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         const bool use_prio = kPrio && mine >= TSDF_PRIO_MIN;  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
         if (use_prio) __builtin_amdgcn_s_setprio(3);
-        for (;;) {
+        // Each wave takes its next item (and issues the load of its list entry) before it
+        // integrates the current one, so the entry's latency overlaps the current item instead of
+        // stalling the next one's start (one item held in reserve per wave).
+        const auto take = [&](ListEntry& e, int& zoff) -> bool {
             unsigned j = 0;
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
@@ -1329,15 +1350,28 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             // taken one after the other, so they run side by side on the workgroup's waves and
             // share their depth / colour gathers in the CU's cache
             const long long k = (long long)wg + (long long)(j / parts) * n_wg;  // increasing for this wave
-            if (k >= (long long)total) break;
+            if (k >= (long long)total) return false;
             while (c > 0 && (unsigned)k - k0 >= nc) {
                 k0 += nc;
                 --c;
                 nc = min(coh_load(&count[c + 1]), nbk);
             }
+            e = list[(size_t)c * nbk + ((unsigned)k - k0)];
+            zoff = (int)(j % parts) * NZ;
+            return true;
+        };
+        ListEntry e = 0;
+        int zoff = 0;
+        bool have = take(e, zoff);
+        while (have) {
+            ListEntry en = 0;
+            int zn = 0;
+            const bool more = take(en, zn);
             // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + ((unsigned)k - k0)],
-                                                   (int)(j % parts) * NZ, s_stat, s_rcp, nupd, res);
+            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, res);
+            have = more;
+            e = en;
+            zoff = zn;
         }
         if (use_prio) __builtin_amdgcn_s_setprio(0);
         return;

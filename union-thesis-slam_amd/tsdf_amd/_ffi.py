@@ -84,6 +84,7 @@ SIGNATURES = {
     "tsdf_dense_get": [_P, _P, _P, _P],
     "tsdf_dense_set": [_P, _P, _P, _P],
     "tsdf_dense_sync": [_P],
+    "tsdf_dense_frames_per_launch": [_P, _P],
     "tsdf_dense_stats": [_P, _P, _I],
     "tsdf_dense_set_profiling": [_P, _I],
     "tsdf_hash_create": [_P, _P, _D, _D, _I64, _I64, _I, _I, _I, _I, _P],

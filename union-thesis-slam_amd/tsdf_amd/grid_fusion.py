@@ -193,6 +193,12 @@ class TSDFVolume:
     def sync(self):
         _ffi.call("tsdf_dense_sync", self._h)
 
+    def frames_per_launch(self):
+        """Frames one launch integrates (the temporal batch, tsdf_dense_frames_per_launch)."""
+        n = ctypes.c_int(0)
+        _ffi.call("tsdf_dense_frames_per_launch", self._h, ctypes.byref(n))
+        return n.value
+
     def stats(self, reset=False):
         s = _ffi.Stats()
         _ffi.call("tsdf_dense_stats", self._h, ctypes.byref(s), int(bool(reset)))
