@@ -414,6 +414,9 @@ def main():
         dh = depth[:ni].cpu().numpy().view(np.uint16)
         ch = rgb[:ni].cpu().numpy()
         vol.set_profiling(False)
+        # one untimed launch's worth first: the handle allocates its page-locked bounce slots and
+        # device staging slots at its first host-frame call (a one-time cost, not the rate)
+        vol.integrate_batch(dh[:BATCH], ch[:BATCH], K, Tinv[:BATCH], sync=True)
         barrier()
         sync()
         t0 = time.perf_counter()

@@ -388,7 +388,7 @@ int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, con
         if (flags & TSDF_DEVICE_PTRS) return set_error(TSDF_E_ARG, "TSDF_DEFER takes host frames only");
         if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(dense_flush(h));
         TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, obs_weight));
-        if (B.dfr.n == B.batch) TSDF_TRY(dense_flush(h));
+        if (B.dfr.n == B.defer_frames) TSDF_TRY(dense_flush(h));
         return TSDF_OK;
     }
     TSDF_TRY(dense_flush(h));

@@ -1304,7 +1304,7 @@ int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const
         if (h->pend.on && !B.stage_fits(depth_kind, color_kind, height, width)) TSDF_TRY(hash_settle(h));
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1
         TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0));
-        if (B.dfr.n == B.batch) TSDF_TRY(hash_flush(h, false));
+        if (B.dfr.n == B.defer_frames) TSDF_TRY(hash_flush(h, false));
         return TSDF_OK;
     }
     TSDF_TRY(hash_flush(h));

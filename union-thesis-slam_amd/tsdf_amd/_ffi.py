@@ -129,7 +129,10 @@ def load(path: str = LIB_PATH):
             "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:  # an older build under A/B (TSDF_HIP_LIB): calling it fails loudly
+            continue
         fn.argtypes = args
         fn.restype = ctypes.c_int
     for name in ("tsdf_last_error", "tsdf_build_id"):

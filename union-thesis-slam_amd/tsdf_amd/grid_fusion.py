@@ -195,6 +195,8 @@ class TSDFVolume:
 
     def frames_per_launch(self):
         """Frames one launch integrates (the temporal batch, tsdf_dense_frames_per_launch)."""
+        if not hasattr(_ffi.load(), "tsdf_dense_frames_per_launch"):  # (an older build under A/B)
+            return 8
         n = ctypes.c_int(0)
         _ffi.call("tsdf_dense_frames_per_launch", self._h, ctypes.byref(n))
         return n.value
