@@ -247,6 +247,9 @@ int tsdf_hash_sync(tsdf_hash_t* h);
 int tsdf_hash_trim(tsdf_hash_t* h);
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);
+/* Frames one launch of this table integrates (as tsdf_dense_frames_per_launch: 16 in this build;
+ * shards of n_shards > 1 always kMaxBatch). */
+int tsdf_hash_frames_per_launch(tsdf_hash_t* h, int* n);
 
 /* ---- frame utilities ---------------------------------------------------------------------
  * Volume bounds from view frustums: the demo loop grid_demo1.py:50-64 (hash_demo1.py:93-107)

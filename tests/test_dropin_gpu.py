@@ -131,6 +131,49 @@ def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe, vmm):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("max_load", [None, "0.97"])
+def test_async_hash_table_grows_before_the_launches_in_flight_fill_it(monkeypatch, max_load):
+    """The load-factor sweep's policy run (tools/hash_sweep.py; it skipped bricks in round 4): a
+    2^17-slot table, asynchronous calls over the bench ring's 1000 frames.  The table must double
+    before the two launches in flight can fill its slots -- under the reference's 0.75 policy
+    (growth can jump just below the threshold) and with the policy lifted to 0.97 -- so no brick
+    is skipped, and the result equals the dense grid."""
+    import torch
+    from tsdf_amd import grid_fusion, hash_fusion, scene
+    if max_load:
+        monkeypatch.setenv("TSDF_HASH_MAX_LOAD", max_load)
+    n = 1000
+    poses = scene.trajectory(n, seed=0, radius_frac=scene.BENCH_RING)
+    sph = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
+    dev = torch.device("cuda", 0)
+    depth = torch.empty((n, 480, 640), dtype=torch.int16, device=dev)
+    rgb = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
+    for s in range(0, n, 50):
+        d, c = scene.render(poses[s:s + 50], sph, seed=0, start=s, device=dev, depth_dtype=torch.int16)
+        depth[s:s + len(d)] = d
+        rgb[s:s + len(c)] = c
+    torch.cuda.synchronize()
+    K = scene.intrinsics()
+    Tinv = np.linalg.inv(poses)
+    h = hash_fusion.HashTable(np.array(BNDS), 0.02, 1 << 17, max_blocks=1 << 15)
+    # (a fresh table's first batch runs synchronously -- explicitly here -- and its pool overflow
+    # re-runs exactly; bricks_skipped counts those re-run bricks too)
+    nb = h.frames_per_launch()
+    h.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv[:nb], hw=(480, 640), device_ptrs=True)
+    skipped0 = h.stats()["bricks_skipped"]
+    h.integrate_batch(depth[nb:].data_ptr(), rgb[nb:].data_ptr(), K, Tinv[nb:], hw=(480, 640), device_ptrs=True,
+                      sync=False)
+    h.sync()  # (raises TSDF_E_CAPACITY if an asynchronous launch skipped a brick)
+    assert h.stats()["bricks_skipped"] == skipped0
+    info = h.info()
+    assert info["capacity"] > 1 << 17 and info["used"] > 100_000
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.02)
+    g.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True)
+    del depth, rgb
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
+
+
 def test_deferred_hash_restage_after_a_pending_overflow():
     """Round-2 advisor finding: a per-frame call that fills a batch launches it and leaves its
     overflow check (grow, exact re-run of the skipped bricks) to the next call; that re-run reads

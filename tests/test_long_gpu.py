@@ -3,8 +3,9 @@
   * config[3] per rank: cyclic column shard 3 of 8 of the 512^3 @ 2 cm volume over 1000 frames
     of the bench trajectory, bit-exact against the oracle on rows of the shard; and over 5000
     frames, where weights cross the LDS reciprocal table's limit by accumulation;
-  * the fast-path boundaries: weights around the 4087 limit of the LDS part of the reciprocal
-    table and the 65527 limit of the whole table (kRcpTab / kRcpBig, csrc/tsdf_device.h) and
+  * the fast-path boundaries: weights around the 4079 limit of the LDS part of the reciprocal
+    table and the 65519 limit of the whole table (kRcpTab / kRcpBig less kMaxBatch + 1 = 17,
+    csrc/tsdf_device.h; the preloaded ranges also straddle 4087 / 65527 of -DTSDF_MAX_BATCH=8) and
     non-canonical colours, preloaded with set_state;
   * config[4] per rank: bucket-range hash shard 5 of 8 over a 1024^3 @ 1 cm extent with 2^22
     buckets over 500 frames, against dense slabs (and the oracle) on rows restricted to the
@@ -76,9 +77,9 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
 def test_config3_rank_shard_10000_frames_full_sequence():
     """config[3]'s whole sequence on one rank (BASELINE: 10k frames; the demo loop is
     grid_demo1.py:76-87): cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 10,000 frames of
-    the bench trajectory (1250 batches through the pipelined launches).  Weights pass the 4087
+    the bench trajectory (625 16-frame batches through the pipelined launches).  Weights pass the 4079
     limit of the LDS part of the reciprocal table by accumulation alone (no preload), so waves
-    move to the HBM table mid-run, and stay below the whole table's 65527.  The two rows holding
+    move to the HBM table mid-run, and stay below the whole table's 65519.  The two rows holding
     the largest weights equal the oracle bit for bit; the frames stay in HBM (15 GB) and reach
     the host in chunks for the oracle."""
     import torch
@@ -103,7 +104,7 @@ def test_config3_rank_shard_10000_frames_full_sequence():
     xi = sharding.columns(3, 8, 512)
     _, W, _ = vol.get_state()
     row_max = W.reshape(len(xi), -1).max(1)
-    assert 4087 < row_max.max() < 65527
+    assert 4087 < row_max.max() < 65519
     pick = np.argsort(row_max)[-2:]  # the two rows with the largest weights
     rows = xi[np.sort(pick)]
     del W
@@ -119,11 +120,11 @@ def test_config3_rank_shard_10000_frames_full_sequence():
     assert vol.stats()["frames"] == n
 
 
-@pytest.mark.parametrize("batched,w_lo,limit", [(False, 4078, 4087), (True, 4078, 4087),
-                                                (True, 65515, 65527)])
+@pytest.mark.parametrize("batched,w_lo,limit", [(False, 4078, 4079), (True, 4078, 4079),
+                                                (True, 65515, 65519)])
 def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched, w_lo, limit):
     """Preloaded weights around a limit of the RN(1/n) table (its LDS part covers integer weights
-    below 4087, then waves read the HBM part; past 65527 the quotients switch to IEEE division)
+    below 4079, then waves read the HBM part; past 65519 the quotients switch to IEEE division)
     and colours that are not the canonical B*65536+G*256+R integers (non-integral, negative,
     >= 2^24), next to canonical ones: every path of the update equals the oracle bit for bit."""
     from tsdf_amd import grid_fusion, scene

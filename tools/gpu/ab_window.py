@@ -17,9 +17,6 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(REPO, "union-thesis-slam_amd"))
 from tsdf_amd import _ffi, grid_fusion, hash_fusion, scene  # noqa: E402
 
-B = 8
-
-
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     name = sys.argv[2] if len(sys.argv) > 2 else os.path.basename(_ffi.LIB_PATH)
@@ -60,6 +57,8 @@ def main():
     out = {"lib": name, "build_id": _ffi.build_id()}
     bnds = np.array([[0.0, 10.24]] * 3)
     vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02)
+    B = vol.frames_per_launch()  # a step = one launch's frames, as in bench.py
+    out["frames_per_launch"] = B
     rows = []
     for _ in range(reps):
         vol.reset()

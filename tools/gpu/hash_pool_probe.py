@@ -3,7 +3,10 @@ table, 5 synchronous warm-up batches, 20 timed asynchronous batches) with the be
 (2^15 blocks, grown by mapping during the window) against a pool mapped for every brick of the
 volume from the start (2^18: no growth), each three times, after a clock warm-up.
 
-    PYTHONPATH=union-thesis-slam_amd python tools/gpu/hash_pool_probe.py
+    PYTHONPATH=union-thesis-slam_amd python tools/gpu/hash_pool_probe.py [premapped]
+
+(premapped: the second configuration only -- with TSDF_HASH_VMM=0, plain allocations against the
+reserved-and-mapped ranges, the same pool size)
 """
 import contextlib
 import io
@@ -42,7 +45,12 @@ def main():
         vol.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv[:160], hw=(480, 640), device_ptrs=True)
     vol.close()
     out = {}
-    for name, mb in (("pool_2^15_grown", 1 << 15), ("pool_2^18_premapped", 1 << 18)):
+    cfgs = (("pool_2^15_grown", 1 << 15), ("pool_2^18_premapped", 1 << 18))
+    if sys.argv[1:] == ["premapped"]:
+        cfgs = cfgs[1:]
+    tag = "vmm" if os.environ.get("TSDF_HASH_VMM", "1") != "0" else "plain"
+    for name, mb in cfgs:
+        name = f"{name}_{tag}"
         rows = []
         for _ in range(3):
             with contextlib.redirect_stdout(io.StringIO()):

@@ -101,12 +101,22 @@ static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
 #define TSDF_FULL_BATCH TSDF_MAX_BATCH
 #endif
 constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxBatch;
+// integrate_items / integrate_brick options (A/B builds)
+#ifndef TSDF_XCD_DEAL  // deal list items to workgroups XCD by XCD (integrate_items)
+#define TSDF_XCD_DEAL 0
+#endif
+#ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
+#define TSDF_ITEM_PREFETCH 1
+#endif
+#ifndef TSDF_RES_PREFETCH  // hash: read the claim word with the item's first instructions
+#define TSDF_RES_PREFETCH 1
+#endif
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
 constexpr int kCountWords = 32, kDoneWord = 24;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 // The whole table in HBM (512 KB, L2-resident) for waves with a weight past the LDS part (long
-// runs: weights pass 4087 after ~4300 frames of a room seen from inside); 65536 keeps every colour
+// runs: weights pass 4079 after ~4300 frames of a room seen from inside); 65536 keeps every colour
 // numerator w*c + c' below 2^24 (exact in f32).
 constexpr int kRcpBig = 65536;
 
@@ -691,7 +701,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const double* const rcp_hbm = v.rcp;
     const bool canon = v.canon != 0;
     [[maybe_unused]] int cur_pref = kResFree;
-    if constexpr (kHalfHash)  // (issued now, waited for where it is used; the bound check is below)
+    if constexpr (kHalfHash && TSDF_RES_PREFETCH)  // (issued now, waited for where it is used; the bound check is below)
         cur_pref = b < v.nb[0] * v.nb[1] * v.nb[2] ? __hip_atomic_load(res + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
                                                    : kResFree;
     const int nb12 = v.nb[1] * v.nb[2];
@@ -729,7 +739,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // ordering); a negative value or a block this launch inserted (kResNew) is read again with
         // acquire semantics
         int cur = cur_pref;
-        if (cur < 0 || (cur & kResNew)) cur = res_load(rp);
+        if (!TSDF_RES_PREFETCH || cur < 0 || (cur & kResNew)) cur = res_load(rp);
         if (cur >= 0) {
         } else if (zoff == 0) {  // not found by the cull: the z-low wave looks again, for both halves
             long long slot = 0, probe = 0;
@@ -862,7 +872,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             }
             // Fast paths (wave-uniform; weights grow by one per frame, so the limits leave room
             // for a whole batch): every lane's weights are small integers -> RN(1/wn) from the LDS
-            // table and Markstein quotients; past the LDS part (a weight of the wave >= 4087) the
+            // table and Markstein quotients; past the LDS part (a weight of the wave >= 4079) the
             // same from the HBM table; and, for RGB8 frames, every colour is canonical (an integer
             // B*65536+G*256+R < 2^24) -> the same for the three colour channels, in f32 with
             // RN32(1/wn) = f32(RN64(1/wn)) (checked for every table entry by the CPU tests).
@@ -1325,13 +1335,20 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // shard (~15 items per workgroup), so only for workgroups with many items; dense: neutral
         // on one GPU, -2 % on an eighth shard, so off.
         constexpr bool kPrio = HASH ? TSDF_PRIO_HASH != 0 : TSDF_PRIO != 0;
+#if TSDF_XCD_DEAL
+        // XCD-aware dealing: the launch's workgroups go to the 8 XCDs round-robin (workgroup w on
+        // XCD w % 8), so dealing brick k to workgroup k mod n_wg would hand each XCD every 8th
+        // brick of the list, spread over the whole image.  Renumbered, workgroup w deals as
+        // (w % 8) * n_wg/8 + w / 8: each XCD takes runs of n_wg/8 consecutive bricks (neighbours
+        // in the cull's order), whose gathers share its L2.
+        if ((n_wg & 7) == 0) wg = (wg & 7) * (n_wg >> 3) + (wg >> 3);
+#endif
         const unsigned mine = total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
         const bool use_prio = kPrio && mine >= TSDF_PRIO_MIN;  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
         if (use_prio) __builtin_amdgcn_s_setprio(3);
-        // Each wave takes its next item (and issues the load of its list entry) before it
-        // integrates the current one, so the entry's latency overlaps the current item instead of
-        // stalling the next one's start (one item held in reserve per wave).
+        // (TSDF_ITEM_PREFETCH: each wave takes its next item, and issues the load of its list
+        // entry, before it integrates the current one -- one item held in reserve per wave)
         const auto take = [&](ListEntry& e, int& zoff) -> bool {
             unsigned j = 0;
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
@@ -1362,6 +1379,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         };
         ListEntry e = 0;
         int zoff = 0;
+#if TSDF_ITEM_PREFETCH
         bool have = take(e, zoff);
         while (have) {
             ListEntry en = 0;
@@ -1373,6 +1391,10 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             e = en;
             zoff = zn;
         }
+#else
+        while (take(e, zoff))  // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
+            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, res);
+#endif
         if (use_prio) __builtin_amdgcn_s_setprio(0);
         return;
     }

@@ -809,6 +809,11 @@ int async_room(tsdf_hash* h, long long s) {
     if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, pool_target(h, need + step)));
     while ((double)(used + 3 * h->recent_growth() + h->tomb_est) >= h->max_load * (double)h->map_size)
         TSDF_TRY(grow_table(h));
+    // ... and the table's slots, whatever the load-factor policy allows (TSDF_HASH_MAX_LOAD up to
+    // 0.99, or a jump in growth just below 0.75): the same two lists' worth of new keys must fit
+    // below 31/32 of the slots, or launch s could find the table full and skip bricks
+    const long long burst = std::max<long long>(3 * h->recent_growth(), 2 * r.listed + h->recent_growth());
+    while (used + h->tomb_est + burst >= h->t.capacity - h->t.capacity / 32) TSDF_TRY(grow_table(h));
     return TSDF_OK;
 }
 
@@ -1536,6 +1541,12 @@ int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset) {
     TSDF_HIP(hipSetDevice(h->b.device));
     TSDF_TRY(hash_flush(h));
     return h->b.read_stats(out, reset);
+}
+
+int tsdf_hash_frames_per_launch(tsdf_hash_t* h, int* n) {
+    if (!h || !n) return set_error(TSDF_E_ARG, "null pointer");
+    *n = h->b.batch;
+    return TSDF_OK;
 }
 
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on) {

@@ -97,6 +97,7 @@ SIGNATURES = {
     "tsdf_hash_remove": [_P, _P, _I64, _P],
     "tsdf_hash_resize": [_P, _I64],
     "tsdf_hash_info": [_P, _P],
+    "tsdf_hash_frames_per_launch": [_P, _P],
     "tsdf_hash_get_dense": [_P, _P, _P, _P],
     "tsdf_hash_to_dense": [_P, _P],
     "tsdf_hash_trim": [_P],

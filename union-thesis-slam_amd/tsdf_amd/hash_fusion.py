@@ -75,6 +75,14 @@ class HashTable:
     def _table_size(self) -> int:
         return self.info()["capacity"]
 
+    def frames_per_launch(self):
+        """Frames one launch integrates (the temporal batch, tsdf_hash_frames_per_launch)."""
+        if not hasattr(_ffi.load(), "tsdf_hash_frames_per_launch"):  # (an older build under A/B)
+            return 8
+        n = ctypes.c_int(0)
+        _ffi.call("tsdf_hash_frames_per_launch", self._h, ctypes.byref(n))
+        return n.value
+
     def info(self) -> dict:
         s = _ffi.HashInfo()
         _ffi.call("tsdf_hash_info", self._h, ctypes.byref(s))
