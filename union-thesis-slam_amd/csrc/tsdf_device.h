@@ -105,11 +105,12 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_XCD_DEAL  // deal list items to workgroups XCD by XCD (integrate_items)
 #define TSDF_XCD_DEAL 0
 #endif
+// (both measured neutral to -1.2 % at the driver window, profiles/r04_h2/ab.jsonl: off)
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
-#define TSDF_ITEM_PREFETCH 1
+#define TSDF_ITEM_PREFETCH 0
 #endif
 #ifndef TSDF_RES_PREFETCH  // hash: read the claim word with the item's first instructions
-#define TSDF_RES_PREFETCH 1
+#define TSDF_RES_PREFETCH 0
 #endif
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
@@ -1604,8 +1605,8 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
 #ifndef TSDF_FUSED_WG
 #define TSDF_FUSED_WG 768  // dense: 12 waves, 2 per CU at 6 waves/SIMD (+0.8 % over 512)
 #endif
-#ifndef TSDF_FUSED_HASH_WG
-#define TSDF_FUSED_HASH_WG 512
+#ifndef TSDF_FUSED_HASH_WG  // hash: 768 too (12 waves, 2 per CU): -3.6 % per launch against 512 on
+#define TSDF_FUSED_HASH_WG 768  // the 250-step window, even on the driver window (profiles/r04_h2/)
 #endif
 constexpr int kFusedWG = TSDF_FUSED_WG, kFusedHashWG = TSDF_FUSED_HASH_WG;
 static_assert(kFusedWG >= kCullWG && kFusedHashWG >= kCullWG && kFusedWG % 64 == 0 && kFusedHashWG % 64 == 0,
