@@ -4,15 +4,10 @@
 # waves/SIMD), and the hash pool on mapped ranges against plain allocations.
 set -o pipefail
 R=$(pwd)
-O="$R/gpurun_out/r04_h"
+O="$R/gpurun_out/r04_h2"
 mkdir -p "$O"
 export PYTHONPATH="$R/union-thesis-slam_amd"
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_dropin_gpu.py \
-  -k "table_grows or turn_into or grows_ahead" > "$O/tests.txt" 2>&1 || exit $?
-# (the same test on the build before the fix, informational: does its table fill?)
-TSDF_HIP_LIB=$R/abtest/libr4l.so timeout -k 10 300 python -u -m pytest -x -v --timeout 250 --timeout-method thread \
-  tests/test_dropin_gpu.py -k "table_grows" > "$O/tests_r4l.txt" 2>&1
-rc=$?; echo "rc=$rc" >> "$O/tests_r4l.txt"; [ $rc -le 1 ] || exit $rc
+# (the tests and the pre-fix control ran in the first attempt: gpurun_out/r04_h/tests*.txt)
 timeout -k 10 500 python -u tools/hash_sweep.py > "$O/hash_sweep.json" 2> "$O/hash_sweep.err" || exit $?
 for rep in 1 2; do
   for n in cur p0 p0r0 b16 p0w768 p0hw5; do

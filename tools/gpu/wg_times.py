@@ -17,7 +17,7 @@ from tsdf_amd import _ffi, grid_fusion, scene  # noqa: E402
 
 def main():
     dev = torch.device("cuda", 0)
-    F = 200
+    F = 400
     poses = scene.trajectory(F, seed=0, radius_frac=scene.BENCH_RING)
     sph = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
     depth = torch.empty((F, 480, 640), dtype=torch.int16, device=dev)
@@ -38,10 +38,11 @@ def main():
     for world in (1, 2, 4, 8):
         vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(0, world))
         rows = []
-        for start in range(0, 192, 32):  # 4 batches a call: its launch 1 runs all three stages
-            vol.integrate_batch(depth.data_ptr() + start * ds, rgb.data_ptr() + start * cs, K, Tinv[start:start + 32],
-                                hw=(480, 640), device_ptrs=True)
-            if start < 64:
+        B = vol.frames_per_launch()
+        for start in range(0, F - 4 * B + 1, 4 * B):  # 4 batches a call: its launch 1 runs all three stages
+            vol.integrate_batch(depth.data_ptr() + start * ds, rgb.data_ptr() + start * cs, K,
+                                Tinv[start:start + 4 * B], hw=(480, 640), device_ptrs=True)
+            if start == 0:
                 continue
             fn(buf.ctypes.data)
             t0 = buf[0].astype(np.int64)

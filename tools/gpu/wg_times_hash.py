@@ -1,7 +1,7 @@
 """Where the time of a fused launch goes, hash against dense, on one GPU (diagnostic build:
 tools/build_variant.sh wgt "-DTSDF_WG_TIMES", run with TSDF_HIP_LIB=abtest/libwgt.so).  The bench's
-driver window (frames 40-199 after 40 warm-up frames, 4-batch calls: the second launch of each call
-runs all three stages) into a fresh dense volume, a fresh hash table (inserting) and the same hash
+driver window (a fresh volume / table, 5 batches, then calls of 4 batches: the second launch of each
+call runs all three stages) into a fresh dense volume, a fresh hash table (inserting) and the same hash
 table again (every block exists).  Per role: workgroups, first / last start, median / last end,
 mean busy time (us from the launch's first workgroup start).  One JSON line per configuration.
 
@@ -45,7 +45,7 @@ def summarize(buf):
 
 def main():
     dev = torch.device("cuda", 0)
-    F = 200
+    F = 400
     poses = scene.trajectory(F, seed=0, radius_frac=scene.BENCH_RING)
     sph = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
     depth = torch.empty((F, 480, 640), dtype=torch.int16, device=dev)
@@ -65,10 +65,11 @@ def main():
     buf = np.zeros((3, NW), np.uint64)
 
     def run(kind, v, label):
-        v.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv[:40], hw=(480, 640), device_ptrs=True)
+        B = v.frames_per_launch()
+        v.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv[:5 * B], hw=(480, 640), device_ptrs=True)
         rows = []
-        for start in range(40, 200, 32):
-            v.integrate_batch(depth.data_ptr() + start * ds, rgb.data_ptr() + start * cs, K, Tinv[start:start + 32],
+        for start in range(5 * B, 25 * B - 4 * B + 1, 4 * B):  # 4 batches a call: launch 1 runs all three stages
+            v.integrate_batch(depth.data_ptr() + start * ds, rgb.data_ptr() + start * cs, K, Tinv[start:start + 4 * B],
                               hw=(480, 640), device_ptrs=True, sync=False)
             v.sync()
             fns[kind](buf.ctypes.data)
@@ -95,6 +96,11 @@ def main():
         ht = hash_fusion.HashTable(bnds.copy(), 0.02, 1 << 22, max_blocks=1 << 15)
     run("hash", ht, "hash, driver window, fresh table (inserting)")
     run("hash", ht, "hash, driver window again (every block exists)")
+    ht.close()
+    with contextlib.redirect_stdout(io.StringIO()):
+        ht = hash_fusion.HashTable(bnds.copy(), 0.02, 1 << 22, shard=0, n_shards=8, max_blocks=1 << 15)
+    run("hash", ht, "hash bucket-range shard 0 of 8, fresh (inserting)")
+    run("hash", ht, "hash bucket-range shard 0 of 8 again (every block exists)")
     ht.close()
 
 

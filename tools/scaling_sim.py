@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--only", default=None, help="W:R -- time only rank R of world W (for profiling)")
     ap.add_argument("--hash", action="store_true", help="bucket-range hash shards instead of dense columns")
     ap.add_argument("--extent", type=int, default=512, help="hash: 512 (2 cm) or 1024 (1 cm) voxels per axis")
+    ap.add_argument("--kernel-time", action="store_true", help="also time the integrate launches (HIP events)")
     a = ap.parse_args()
     import torch
     from tsdf_amd import grid_fusion, scene, sharding
@@ -72,9 +73,15 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(r, world))
         timed(vol, 0, a.warmup)
+        vol.set_profiling(a.kernel_time)
         vol.stats(reset=True)
         t = timed(vol, a.warmup, a.steps)
-        print(json.dumps({"only": a.only, "fps": round(a.steps / t, 1), "stats": vol.stats()}, default=float))
+        st = vol.stats()
+        r = {"only": a.only, "fps": round(a.steps / t, 1), "stats": st}
+        if a.kernel_time:
+            r["kernel_avg_us"] = round(1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), 2)
+            r["launches"] = st["kernel_launches"]
+        print(json.dumps(r, default=float))
         return
     for world in [int(w) for w in a.worlds.split(",")]:
         for mode in ("slab", "cyclic"):
@@ -121,9 +128,13 @@ def hash_shards(a, timed, bnds):
                 ht = hash_fusion.HashTable(bnds.copy(), vs, 1 << 22, shard=r, n_shards=world,
                                            max_blocks=1 << 15)
             timed(ht, 0, a.warmup)
+            ht.set_profiling(a.kernel_time)
             ht.stats(reset=True)
             t = timed(ht, a.warmup, a.steps)
             st = ht.stats()
+            ht.stats(reset=True)
+            t2 = timed(ht, a.warmup, a.steps)  # the same window again: every block exists
+            st2 = ht.stats()
             ht.trim()  # the pool at its live blocks (the run's growth headroom handed back)
             info = ht.info()
             state = info["slots"] * 12 + info["pool_capacity"] * per_block
@@ -132,7 +143,12 @@ def hash_shards(a, timed, bnds):
                         "blocks_live": info["used"], "pool_capacity": info["pool_capacity"],
                         "hbm_state_bytes": state,
                         "dense_shard_bytes": 12 * a.extent ** 3 // world,
-                        "bricks_skipped": st["bricks_skipped"]})
+                        "bricks_skipped": st["bricks_skipped"], "blocks_allocated": st["blocks_allocated"]})
+            res[-1]["no_alloc_repeat"] = {"fps": round(a.steps / t2, 1), "blocks_allocated": st2["blocks_allocated"]}
+            if a.kernel_time:
+                res[-1]["kernel_avg_us"] = round(1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), 2)
+                res[-1]["launches"] = st["kernel_launches"]
+                res[-1]["no_alloc_repeat"]["kernel_avg_us"] = round(1e3 * st2["kernel_ms"] / max(1, st2["kernel_launches"]), 2)
             print(json.dumps(res[-1]), file=sys.stderr, flush=True)
             ht.close()
             del ht

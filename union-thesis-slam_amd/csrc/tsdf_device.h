@@ -102,8 +102,8 @@ static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
 #endif
 constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxBatch;
 // integrate_items / integrate_brick options (A/B builds)
-#ifndef TSDF_XCD_DEAL  // deal list items to workgroups XCD by XCD (integrate_items)
-#define TSDF_XCD_DEAL 0
+#ifndef TSDF_XCD_DEAL  // deal list items to workgroups XCD by XCD (integrate_items): dense -1.5 %,
+#define TSDF_XCD_DEAL 1  // hash -1 % per launch, hash eighth shard +3 % (profiles/r04_i/)
 #endif
 // (both measured neutral to -1.2 % at the driver window, profiles/r04_h2/ab.jsonl: off)
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
