@@ -102,6 +102,9 @@ static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
 #endif
 constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxBatch;
 // integrate_items / integrate_brick options (A/B builds)
+#ifndef TSDF_OCC_RMW  // hash z-half waves: entry words read at item start, stored if changed
+#define TSDF_OCC_RMW 0
+#endif
 #ifndef TSDF_XCD_DEAL  // deal list items to workgroups XCD by XCD (integrate_items): dense -1.5 %,
 #define TSDF_XCD_DEAL 1  // hash -1 % per launch, hash eighth shard +3 % (profiles/r04_i/)
 #endif
@@ -665,6 +668,15 @@ __device__ inline double dist_of(double trunc, double rtrunc, double diff) {
 //    at item start stays missing until one of its own halves inserts it.)
 // Both waves share a workgroup, so workgroup-scope ordering suffices (agent scope would write
 // back and invalidate the XCD's L2 at every claim).
+#ifdef TSDF_HASH_DIAG
+// Diagnostic builds only (tools/gpu/hash_diag.py): counts of the z-half protocol's events, summed
+// over launches: 0 items, 1 z-low re-lookups, 2 of them found, 3 z-high waits at start, 4 their
+// sleep iterations, 5 end claims (inserts), 6 end waits for the claimer, 7 their sleep iterations
+__device__ unsigned long long g_hash_diag[8];
+#define TSDF_HDIAG(i, n) (lane_id() == 0 ? (void)atomicAdd(&g_hash_diag[i], (unsigned long long)(n)) : (void)0)
+#else
+#define TSDF_HDIAG(i, n) ((void)0)
+#endif
 constexpr int kResFree = -1, kResBusy = -2, kResFail = -3, kResMissing = -4;
 constexpr int kResNew = 1 << 30;  // published block | kResNew: inserted by this launch (blocks < 2^30)
 
@@ -677,10 +689,19 @@ __device__ inline void res_publish(int* rp, int val) {  // lane 0, after the wav
 }
 __device__ inline int res_wait(const int* rp, int busy) {  // the published value once not `busy`
     int cur = res_load(rp);
+#ifdef TSDF_HASH_DIAG
+    unsigned spins = 0;
+#endif
     while (cur == busy) {
         __builtin_amdgcn_s_sleep(1);
         cur = res_load(rp);
+#ifdef TSDF_HASH_DIAG
+        ++spins;
+#endif
     }
+#ifdef TSDF_HASH_DIAG
+    TSDF_HDIAG(busy == kResFree ? 4 : 7, spins);
+#endif
     return cur;
 }
 
@@ -741,12 +762,15 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // acquire semantics
         int cur = cur_pref;
         if (!TSDF_RES_PREFETCH || cur < 0 || (cur & kResNew)) cur = res_load(rp);
+        TSDF_HDIAG(0, 1);
         if (cur >= 0) {
         } else if (zoff == 0) {  // not found by the cull: the z-low wave looks again, for both halves
             long long slot = 0, probe = 0;
             const int r = table_find_or_insert(tab, pack_key(bx, by, bz), ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits),
                                                false, is_new, slot, probe);
             cur = r >= 0 ? r : kResMissing;
+            TSDF_HDIAG(1, 1);
+            TSDF_HDIAG(2, r >= 0 ? 1 : 0);
             res_publish(rp, cur);
             if (lane == 0) {
                 atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
@@ -754,6 +778,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
             }
         } else {
+            TSDF_HDIAG(3, 1);
             cur = res_wait(rp, kResFree);
         }
         if (cur >= 0) {
@@ -769,6 +794,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }  // else missing (or being claimed / failed): blk stays -1, the frames run from the fresh
            // state (below) and the end of the item claims the block or waits for the claimer
     }
+    // (TSDF_OCC_RMW: the entry words this half owns, loaded now and written back at the end only
+    // if the batch set a new bit -- no atomic: no other wave writes them during the launch)
+    [[maybe_unused]] unsigned long long occ_old = 0;
+    if constexpr (kHalfHash && TSDF_OCC_RMW)
+        if (blk >= 0 && !is_new && lane < NZ) occ_old = coh_load(tab.occ + (size_t)blk * kBrickEdge + zoff + lane);
     float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
@@ -1020,6 +1050,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 cur = old;
             }
             if (old == kResMissing && cur == kResMissing) {  // this wave claimed the word
+                TSDF_HDIAG(5, 1);
                 long long slot = 0, probe = 0;
                 const int r = table_find_or_insert(tab, pack_key(bx, by, bz),
                                                    ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits), true,
@@ -1053,6 +1084,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 }
                 blk = r;
             } else {
+                TSDF_HDIAG(6, 1);
                 cur = res_wait(rp, kResBusy);
                 if (cur == kResFail) return;
                 blk = cur & (kResNew - 1);
@@ -1081,7 +1113,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         if (lane < NZ) {
             unsigned long long* o = tab.occ + (size_t)blk * kBrickEdge + zoff + lane;
             if (is_new) coh_store(o, mine);
-            else if (mine) atomicOr(o, mine);
+            else if (kHalfHash && TSDF_OCC_RMW) {
+                if (mine & ~occ_old) coh_store(o, occ_old | mine);
+            } else if (mine) {
+                atomicOr(o, mine);
+            }
         }
     }
     if (lane == 0) atomicAdd(&s_stat[ST_TOUCHED], 1ull);

@@ -1661,6 +1661,17 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 
 }  // extern "C"
 
+#ifdef TSDF_HASH_DIAG
+// (diagnostic builds) the z-half protocol's event counts (g_hash_diag), read and cleared
+extern "C" int tsdf_diag_hash_counts(unsigned long long* out) {
+    TSDF_HIP(hipDeviceSynchronize());
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hash_diag), sizeof(unsigned long long) * 8));
+    const unsigned long long zero[8] = {};
+    TSDF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_hash_diag), zero, sizeof(zero)));
+    return TSDF_OK;
+}
+#endif
+
 #ifdef TSDF_WG_TIMES
 // (diagnostic builds) the last fused hash launch's per-workgroup start / end / role|items
 extern "C" int tsdf_diag_wg_times_hash(unsigned long long* out) {
