@@ -390,7 +390,7 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "traffic_frac": None,
                 "kernel": "tsdf::k_fused<true, 4, 0>: integrates batch k (and culls k+1, preps k+2 in the "
                           "same launch); bytes = batch k's integrate bytes only (SURVEY §8(d): 24 B per "
-                          "updated voxel + 5 B per pixel, x8 frames)",
+                          f"updated voxel + 5 B per pixel, x{BATCH} frames)",
                 "kernel_avg_us": round(1e6 * avg_s, 2),
                 "bytes_per_launch": round(alg_bytes / st["kernel_launches"]),
                 "launches": st["kernel_launches"],
@@ -652,6 +652,8 @@ def main():
             "mean_voxels_updated_per_frame": round(vox / Kf),
             "clock_warmup_ms": args.preheat_ms,
             "cold_window": cold,
+            # (dispatch-order index of the first timed integrate launch, also without --profile)
+            "first_timed_launch_index": first_timed,
             "hash": hash_res,
             "pcie_inclusive": ingest,
             "broadcast_ingest": bcast,

@@ -37,21 +37,43 @@ def bench_line(path):
         return json.loads([l for l in f if l.startswith("{")][-1])
 
 
+def first_index(line):
+    """The bench line's first_timed_launch_index (top level, or in its roofline block); None for a
+    line without it (a pass run with --no-profile before bench.py printed it at top level)."""
+    if line.get("first_timed_launch_index") is not None:
+        return line["first_timed_launch_index"]
+    return (line.get("roofline") or {}).get("first_timed_launch_index")
+
+
 def timed(rows_by_dispatch, first):
     """rows_by_dispatch: [(dispatch_id, row)] of KERNEL -> the K timed launches, from the index the
-    bench line records (roofline.first_timed_launch_index)."""
+    bench line records.  first None: the dense-only PMC / SQ passes end with the timed call, so its
+    K integrate launches are the process's last K launches of KERNEL (checked by pmc_timed: the two
+    launches before them are the call's pipeline-fill launches, prep / cull only)."""
     rows = sorted(rows_by_dispatch, key=lambda r: r[0])
+    if first is None:
+        first = len(rows) - K
     return rows[first:first + K]
 
 
-def pmc_timed(path, counter, first):
+def pmc_timed(path, counter, first, ids=None):
+    """The counter's values on the K timed launches (summed over dimensions / XCDs); ids: take
+    exactly these dispatches (the timed set found on another counter of the same pass)."""
     per = {}
     for row in csv.DictReader(open(path)):
         if row["Counter_Name"] != counter or KERNEL not in row["Kernel_Name"]:
             continue
         d = int(row["Dispatch_Id"])
         per[d] = per.get(d, 0.0) + float(row["Counter_Value"])  # (summed over dimensions / XCDs)
+    if ids is not None:
+        return [per[d] for d in ids]
     t = timed(list(per.items()), first)
+    if first is None:  # the two launches before the last K must be the pipeline fill (no integrate)
+        rows = sorted(per.items())
+        fill = [v for _, v in rows[-K - 2:-K]]
+        med = statistics.median(v for _, v in t)
+        if len(fill) != 2 or max(fill) > 0.1 * med:
+            raise RuntimeError(f"{path}: the last {K} launches of {KERNEL} are not the timed call")
     return [v for _, v in t]
 
 
@@ -67,7 +89,7 @@ def main(tag):
     # the timed launches' trace rows
     trace = [r for r in csv.DictReader(open(os.path.join(src, "kernel_trace_tsdf.csv")))
              if KERNEL in r["Kernel_Name"]]
-    t = timed([(int(r["Dispatch_Id"]), r) for r in trace], line["roofline"]["first_timed_launch_index"])
+    t = timed([(int(r["Dispatch_Id"]), r) for r in trace], first_index(line))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for _, r in t]
     with open(os.path.join(dst, f"{tag}_timed_launches.csv"), "w") as f:
         f.write(f"# {KERNEL}: the {K} timed integrate launches of bench.py --gpus 1 --steps {K} --warmup {W} "
@@ -78,8 +100,8 @@ def main(tag):
             f.write(f"{d},{r['Start_Timestamp']},{r['End_Timestamp']},{us:.2f}\n")
     pl = bench_line(os.path.join(src, "pmc_FETCH_SIZE.json"))
     pw = bench_line(os.path.join(src, "pmc_WRITE_SIZE.json"))
-    fetch = pmc_timed(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", pl["roofline"]["first_timed_launch_index"])
-    write = pmc_timed(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", pw["roofline"]["first_timed_launch_index"])
+    fetch = pmc_timed(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", first_index(pl))
+    write = pmc_timed(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", first_index(pw))
     sys.path.insert(0, REPO)
     import bench
     fk = statistics.median(fetch) * 1024.0
@@ -103,8 +125,15 @@ def sq(tag):
     names = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
              "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
     pl = bench_line(os.path.join(src, "bench.json"))
-    first = pl["roofline"]["first_timed_launch_index"]
-    med = {c: statistics.median(pmc_timed(os.path.join(src, "pmc_sq.csv"), c, first)) for c in names}
+    first = first_index(pl)
+    # the timed dispatches, found on the VALU instruction count (the fill launches have almost none)
+    per = {}
+    for row in csv.DictReader(open(os.path.join(src, "pmc_sq.csv"))):
+        if row["Counter_Name"] == "SQ_INSTS_VALU" and KERNEL in row["Kernel_Name"]:
+            per[int(row["Dispatch_Id"])] = per.get(int(row["Dispatch_Id"]), 0.0) + float(row["Counter_Value"])
+    pmc_timed(os.path.join(src, "pmc_sq.csv"), "SQ_INSTS_VALU", first)  # (checks the fill launches)
+    ids = [d for d, _ in timed(list(per.items()), first)]
+    med = {c: statistics.median(pmc_timed(os.path.join(src, "pmc_sq.csv"), c, first, ids)) for c in names}
     sys.path.insert(0, REPO)
     import bench
     out = {"kernel": KERNEL, "build_id": pl.get("build_id"), "median_per_launch": med,
