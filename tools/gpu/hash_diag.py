@@ -42,7 +42,7 @@ def main():
     lib = _ffi.load()
     fn = lib.tsdf_diag_hash_counts
     fn.argtypes = [ctypes.c_void_p]
-    buf = np.zeros(8, np.uint64)
+    buf = np.zeros(24, np.uint64)
     with contextlib.redirect_stdout(io.StringIO()):
         ht = hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22, max_blocks=1 << 15)
     B = ht.frames_per_launch()
@@ -59,6 +59,10 @@ def main():
         out = {"window": label, "kernel_avg_us": round(1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), 1),
                "launches": st["kernel_launches"], "blocks_allocated": st["blocks_allocated"]}
         out.update({k: int(v) for k, v in zip(NAMES, buf)})
+        for c, name in enumerate(("found_by_cull", "missing_not_updated", "claimer", "partner_waited",
+                                  "found_after_start_lookup")):
+            n, ticks = int(buf[8 + 2 * c]), int(buf[9 + 2 * c])
+            out[name] = {"items": n, "mean_us": round(ticks / 100.0 / max(1, n), 2)}
         print(json.dumps(out), flush=True)
     ht.close()
 
