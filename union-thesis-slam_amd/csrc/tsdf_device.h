@@ -1291,13 +1291,16 @@ __global__ __launch_bounds__(kCullWG) void k_cull(Vol v, Batch bt, Table tab, Li
 // gives the list length written by k_cull; with count == nullptr the first n_list entries are
 // used (hash overflow re-run).
 #ifndef TSDF_PRIO  // progress priority of the dense integrate's waves (integrate_items)
-#define TSDF_PRIO 0
+#define TSDF_PRIO 1
 #endif
 #ifndef TSDF_PRIO_HASH  // ... and of the hash integrate's
 #define TSDF_PRIO_HASH 1
 #endif
 #ifndef TSDF_PRIO_MIN  // ... for workgroups with at least this many list items (brick parts)
 #define TSDF_PRIO_MIN 64
+#endif
+#ifndef TSDF_PRIO_MIN_HASH  // ... the hash integrate's
+#define TSDF_PRIO_MIN_HASH 16
 #endif
 // A pointer the compiler cannot see through: loads from it are neither merged with loads before
 // it nor speculated out of the conditional blocks that use them.  The fused launches read their
@@ -1368,9 +1371,10 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // its tail alone.  A wave's priority falls as its workgroup's share is taken (3 below 1/2,
         // 2 below 13/16, 1 below 15/16, then 0), so a workgroup that lags keeps the issue slots
         // until it has caught up.  Hash: +4 % on one GPU (z-half waves that wait for their
-        // partner's claim word stop losing the SIMD to older workgroups), but -5 % on an eighth
-        // shard (~15 items per workgroup), so only for workgroups with many items; dense: neutral
-        // on one GPU, -2 % on an eighth shard, so off.
+        // partner's claim word stop losing the SIMD to older workgroups), and with 768-thread
+        // workgroups +5 % on an eighth shard too (~35 items per workgroup; TSDF_PRIO_MIN_HASH 16).
+        // Dense: -2.9 % time per 16-frame launch on one GPU, but +3 % on an eighth shard, so from
+        // 64 items per workgroup (profiles/r04_p/).
         constexpr bool kPrio = HASH ? TSDF_PRIO_HASH != 0 : TSDF_PRIO != 0;
 #if TSDF_XCD_DEAL
         // XCD-aware dealing: the launch's workgroups go to the 8 XCDs round-robin (workgroup w on
@@ -1381,7 +1385,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         if ((n_wg & 7) == 0) wg = (wg & 7) * (n_wg >> 3) + (wg >> 3);
 #endif
         const unsigned mine = total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
-        const bool use_prio = kPrio && mine >= TSDF_PRIO_MIN;  // (wave-uniform)
+        const bool use_prio = kPrio && mine >= (HASH ? TSDF_PRIO_MIN_HASH : TSDF_PRIO_MIN);  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
         if (use_prio) __builtin_amdgcn_s_setprio(3);
         // (TSDF_ITEM_PREFETCH: each wave takes its next item, and issues the load of its list
