@@ -1,0 +1,91 @@
+"""The measurement plumbing on the CPU: bench.py attaches the committed PMC / SQ profiles to its
+roofline block only for the library build and workload they measured, and
+tools/summarize_profile.py picks the K timed integrate launches out of a kernel trace -- by the
+index the bench line records, or (passes run without HIP events) as the process's last K launches
+after the timed call's two pipeline-fill launches."""
+import csv
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture()
+def bench(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    sys.path.insert(0, REPO)
+    import bench as b
+    return b
+
+
+def _roof():
+    return {"bound": "hbm", "achieved": 9000.0, "peak": 8000.0, "frac": 1.125, "kernel_avg_us": 650.0,
+            "bytes_per_launch": 6.0e9, "launches": 20}
+
+
+def _profiles(tmp_path, build, workload):
+    pmc = tmp_path / "pmc.json"
+    sq = tmp_path / "sq.json"
+    pmc.write_text(json.dumps({"build_id": build, "workload": workload, "hbm_bytes_per_launch": 2.2e9}))
+    sq.write_text(json.dumps({"build_id": build, "workload": workload, "valu_busy_per_simd": 0.88,
+                              "median_per_launch": {"SQ_INSTS_VALU": 3.4e8}}))
+    return str(pmc), str(sq)
+
+
+def test_profiles_attach_only_for_the_same_build_and_workload(bench, tmp_path, monkeypatch):
+    st = {"voxel_updates": 20 * 16 * 15_000_000, "kernel_launches": 20}
+    pmc, sq = _profiles(tmp_path, "abc", bench.WORKLOAD)
+    monkeypatch.setattr(bench, "PMC_PROFILE", pmc)
+    monkeypatch.setattr(bench, "SQ_PROFILE", sq)
+    roof = _roof()
+    bench.attach_profiles(roof, st, "abc")
+    assert roof["traffic"] == 2_200_000_000 and roof["bound"] == "valu"
+    assert roof["traffic_frac"] == pytest.approx(2.2e9 / 650e-6 / 8e12, abs=1e-4)
+    assert roof["valu"]["valu_busy"] == 0.88 and "profiles_note" not in roof
+    roof = _roof()
+    bench.attach_profiles(roof, st, "other")  # another build: nothing attached, and said why
+    assert "traffic" not in roof and "valu" not in roof and roof["bound"] == "hbm"
+    assert "measured library build abc, this is other" in roof["profiles_note"]
+    pmc, sq = _profiles(tmp_path, "abc", "another workload")
+    monkeypatch.setattr(bench, "PMC_PROFILE", pmc)
+    monkeypatch.setattr(bench, "SQ_PROFILE", sq)
+    roof = _roof()
+    bench.attach_profiles(roof, st, "abc")
+    assert "traffic" not in roof and "measured another workload" in roof["profiles_note"]
+
+
+def _pmc_csv(path, values, kernel):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for d, v in enumerate(values):
+            for half in (0.5, 0.5):  # (summed over dimensions)
+                w.writerow({"Dispatch_Id": 100 + d, "Kernel_Name": "void " + kernel, "Counter_Name": "FETCH_SIZE",
+                            "Counter_Value": v * half})
+            w.writerow({"Dispatch_Id": 100 + d, "Kernel_Name": "tsdf::k_other", "Counter_Name": "FETCH_SIZE",
+                        "Counter_Value": 1.0})
+
+
+def test_summaries_pick_the_timed_launches(tmp_path):
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import summarize_profile as sp
+    K = sp.K
+    warm = [500.0] * 7
+    timed = [1000.0 + i for i in range(K)]
+    # a pass without HIP events: the timed call is last; its two fill launches come first
+    p = str(tmp_path / "a.csv")
+    _pmc_csv(p, warm + [5.0, 7.0] + timed, sp.KERNEL)
+    assert sp.pmc_timed(p, "FETCH_SIZE", None) == timed
+    # by the bench line's index (here 9: after 7 warm-up and 2 fill launches), whatever follows
+    _pmc_csv(p, warm + [5.0, 7.0] + timed + [500.0] * 3, sp.KERNEL)
+    assert sp.pmc_timed(p, "FETCH_SIZE", 9) == timed
+    # the last K are not preceded by two fill launches: refused
+    _pmc_csv(p, warm + [500.0, 500.0] + timed, sp.KERNEL)
+    with pytest.raises(RuntimeError):
+        sp.pmc_timed(p, "FETCH_SIZE", None)
+    assert sp.first_index({"first_timed_launch_index": 4}) == 4
+    assert sp.first_index({"roofline": {"first_timed_launch_index": 5}}) == 5
+    assert sp.first_index({"roofline": None}) is None
