@@ -16,8 +16,10 @@ ranks is taken.  With N ranks each rank owns the 8-voxel x-columns c with c % N 
 column shards) and integrates every frame into them -- no data-path collective --
 so total work is fixed: "scaling": "strong".
 
-Rank 0 prints ONE JSON line.  `roofline` prices the integrate kernel by SURVEY §8(d)'s
-algorithmic bytes (24 B per updated voxel + 5 B per pixel per frame) over its HIP-event time;
+Rank 0 prints ONE JSON line.  `roofline` prices the integrate launch by SURVEY §8(d)'s bytes with
+temporal batching accounted for (24 B per voxel the launch's batch updates at least once, counted
+on the device, + 5 B per pixel per frame) over its HIP-event time, so it cannot pass 1 by batching;
+the hash leg carries the same block (+ 16 B per touched block);
 `cpu_baseline` is the NumPy restatement of the reference's CPU path (oracle/, pinned to the
 reference fixtures) on a bounded sample, with the host's CPU model and BLAS threads.
 Beside `value`: the hash path, the PCIe-inclusive batch rate, the reference's own per-frame
@@ -48,8 +50,11 @@ WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) int
 # the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), quoted only when
 # their workload AND the build id of the library they measured match the loaded library
 # (tsdf_build_id): DRAM-side traffic (FETCH_SIZE / WRITE_SIZE) and VALU issue (SQ counters)
-PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r04.json")
-SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r04.json")
+PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r05.json")
+SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r05.json")
+HASH_WORKLOAD = ("config[2]: the same frames into a voxel hash over the 512^3 @ 2 cm extent (8^3 blocks, 2^22 "
+                 "slots, pool grown from 2^15 blocks)")
+HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r05.json")  # traffic + SQ of k_fused_hash<0>
 
 
 def log(*a):
@@ -58,8 +63,10 @@ def log(*a):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=250, help="timed steps (batches of 8 frames)")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); default: the launcher's WORLD_SIZE, else 1")
+    ap.add_argument("--steps", type=int, default=250,
+                    help="timed steps (one launch's batch each: TSDFVolume.frames_per_launch() = 16 frames)")
     ap.add_argument("--warmup", type=int, default=12, help="untimed steps")
     ap.add_argument("--frames", type=int, default=1000, help="synthetic frames resident in HBM")
     ap.add_argument("--no-hash", action="store_true")
@@ -106,18 +113,19 @@ def self_launch(args):
     return subprocess.call(cmd, env=env)
 
 
-def attach_profiles(roof, st, build_id):
-    """Attach the committed PMC traffic / SQ issue profiles to the roofline block, only when they
-    measured this workload with this exact library build; otherwise say why they are absent."""
+def attach_profiles(roof, st, build_id, pmc_path, sq_path, workload):
+    """Attach committed PMC traffic / SQ issue profiles to a roofline block, only when they
+    measured this workload with this exact library build; otherwise say why they are absent.
+    pmc_path / sq_path may name the same file (the hash profile holds both)."""
     why = []
-    for path, key in ((PMC_PROFILE, "traffic"), (SQ_PROFILE, "valu")):
+    for path, key in ((pmc_path, "traffic"), (sq_path, "valu")):
         rel = os.path.relpath(path, REPO)
         if not os.path.exists(path):
             why.append(f"{key}: no {rel}")
             continue
         with open(path) as fh:
             p = json.load(fh)
-        if p.get("workload") != WORKLOAD:
+        if p.get("workload") != workload:
             why.append(f"{key}: {rel} measured another workload")
             continue
         if p.get("build_id") != build_id:
@@ -129,6 +137,7 @@ def attach_profiles(roof, st, build_id):
             roof["traffic"] = round(tb)
             # measured DRAM-side bytes over this run's average launch time
             roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            roof["traffic_over_algorithmic"] = round(tb / roof["bytes_per_launch"], 3)
             roof["traffic_source"] = (rel + " (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH "
                                       "doubled per the gfx950 rule; build " + build_id + ")")
         med = p.get("median_per_launch", {})
@@ -138,18 +147,55 @@ def attach_profiles(roof, st, build_id):
                 "valu_busy": p["valu_busy_per_simd"],
                 "valu_wave_insts_per_launch": round(med["SQ_INSTS_VALU"]),
                 "valu_lane_insts_per_voxel_update": round(64.0 * med["SQ_INSTS_VALU"] / vox_launch, 1),
+                "wait_any_frac": p.get("wait_any_frac"),
                 "source": rel + " (rocprofv3 --pmc SQ pass of the same kernel, workload and build; busy = "
                           "SQ_ACTIVE_INST_VALU x 4 / SIMD cycles)"}
-            # the binding resource: the one closer to its peak (VALU issue vs measured DRAM bytes;
-            # the algorithmic bytes count every update's state traffic, which temporal batching
-            # keeps on chip)
-            if roof.get("traffic_frac") is not None and p["valu_busy_per_simd"] > roof["traffic_frac"]:
-                roof["bound"] = "valu"
-                roof["bound_note"] = ("VALU issue-bound: the SIMDs issue VALU in valu_busy of their cycles "
-                                      "while DRAM moves traffic_frac of its peak; achieved/peak/frac are the "
-                                      "algorithmic-bytes HBM roofline of the contract")
+    # the binding resource: VALU issue against the HBM bytes (the algorithmic ones and the measured
+    # DRAM ones; both are below peak when the SIMDs are the limit)
+    v = (roof.get("valu") or {}).get("valu_busy")
+    if v is not None:
+        mem = max(roof["frac"], roof.get("traffic_frac") or 0.0)
+        if v > mem:
+            roof["bound"] = "valu"
+            roof["bound_note"] = ("VALU issue-bound: the SIMDs issue VALU in valu_busy of their cycles while "
+                                  "HBM moves frac (algorithmic) / traffic_frac (measured) of its peak")
     if why:
         roof["profiles_note"] = "; ".join(why)
+
+
+def integrate_roofline(st, frames, kernel, first_timed=None, blocks_touched=None):
+    """HBM roofline of the integrate launches, priced by the bytes a launch must
+    move: each voxel its batch updates at least once is read and written once (24 B: tsdf, weight,
+    colour f32 in and out -- temporal batching keeps it on chip across the batch's frames), plus
+    5 B per pixel per frame of input (u16 depth + RGB8), plus for the hash 16 B per touched block
+    (key + slot value).  Counted on the device (tsdf_stats_t.batch_voxels), so `frac` cannot pass
+    1 by batching.  `per_frame_bytes_frac` keeps the per-frame pricing (24 B per update per frame)
+    as a secondary figure: the state traffic batching avoids."""
+    if not st["kernel_launches"]:
+        return None
+    kernel_s = st["kernel_ms"] / 1e3
+    L = st["kernel_launches"]
+    avg_s = kernel_s / L
+    alg = 24.0 * st["batch_voxels"] + 5.0 * PIX * frames
+    per_frame = 24.0 * st["voxel_updates"] + 5.0 * PIX * frames
+    if blocks_touched is not None:
+        alg += 16.0 * blocks_touched
+        per_frame += 16.0 * blocks_touched
+    ach = alg / kernel_s / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "traffic_frac": None,
+            "kernel": kernel,
+            "bytes_rule": "24 B x U_batch (voxels updated at least once per launch, counted on the device) + "
+                          "5 B x pixels x frames" + (" + 16 B x touched brick halves" if blocks_touched is not None else ""),
+            "kernel_avg_us": round(1e6 * avg_s, 2),
+            "bytes_per_launch": round(alg / L),
+            "batch_voxels_per_launch": round(st["batch_voxels"] / L),
+            "voxel_updates_per_launch": round(st["voxel_updates"] / L),
+            "per_frame_bytes_frac": round(per_frame / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+            "launches": L,
+            # dispatch-order index (0-based, among this process's launches of the fused kernel) of
+            # the first timed integrate launch: tools/summarize_profile.py
+            "first_timed_launch_index": first_timed}
 
 
 def frame_ranges(start, count, F):
@@ -264,11 +310,13 @@ def main():
     import torch
     import torch.distributed as dist
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:  # a launcher without --gpus: its WORLD_SIZE
+        args.gpus = world
     if args.gpus != world:
         log(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE {world} ranks")
         sys.exit(2)
@@ -380,24 +428,10 @@ def main():
     vox = sum_over_ranks(float(st["voxel_updates"]))
     fps = Kf / dt_max
     kernel_s = st["kernel_ms"] / 1e3
-    # roofline of the integrate kernel on this rank: algorithmic bytes / HIP-event time
-    alg_bytes = 24.0 * st["voxel_updates"] + 5.0 * PIX * Kf
-    roof = None
-    if st["kernel_launches"]:
-        avg_s = kernel_s / st["kernel_launches"]
-        ach = alg_bytes / kernel_s / 1e9
-        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "traffic_frac": None,
-                "kernel": "tsdf::k_fused<true, 4, 0>: integrates batch k (and culls k+1, preps k+2 in the "
-                          "same launch); bytes = batch k's integrate bytes only (SURVEY §8(d): 24 B per "
-                          f"updated voxel + 5 B per pixel, x{BATCH} frames)",
-                "kernel_avg_us": round(1e6 * avg_s, 2),
-                "bytes_per_launch": round(alg_bytes / st["kernel_launches"]),
-                "launches": st["kernel_launches"],
-                # dispatch-order index (0-based, among this process's launches of the dense fused
-                # kernel) of the first timed integrate launch: tools/summarize_profile.py
-                "first_timed_launch_index": first_timed}
-        attach_profiles(roof, st, _ffi.build_id())
+    roof = integrate_roofline(st, Kf, "tsdf::k_fused<true, 4, 0>: integrates batch k (and culls k+1, preps k+2 in "
+                                      "the same launch)", first_timed)
+    if roof is not None:
+        attach_profiles(roof, st, _ffi.build_id(), PMC_PROFILE, SQ_PROFILE, WORKLOAD)
     vf_mean = st["voxel_updates"] / Kf
     log(f"[rank {rank}] dense: {Kf} frames in {dt * 1e3:.1f} ms -> {Kf / dt:.0f} frames/s, "
         f"V_f mean {vf_mean:.0f} ({100 * vf_mean / (len(vol.x_index) * X * X):.1f}% of shard), "
@@ -535,7 +569,15 @@ def main():
                     "state_bytes_note": "hash: table keys + slot->block map + block pool (tsdf/weight/"
                                         "colour, entry bits, free list) after the run (HashTable.trim; "
                                         "pool_capacity_in_run: before it, with the growth headroom of the "
-                                        "launches in flight); dense: three f32 arrays of the volume"}
+                                        "launches in flight); dense: three f32 arrays of the volume",
+                    "roofline": None}
+        hroof = integrate_roofline(hs, Kf, "tsdf::k_fused_hash<0>: integrates batch k (find-or-insert of its "
+                                           "blocks), culls k+1 and preps k+2 in the same launch; the window "
+                                           "inserts blocks_allocated_in_window blocks",
+                                   blocks_touched=hs["bricks_touched"])
+        if hroof is not None:
+            attach_profiles(hroof, hs, _ffi.build_id(), HASH_PROFILE, HASH_PROFILE, HASH_WORKLOAD)
+            hash_res["roofline"] = hroof
         log(f"[rank {rank}] hash: {Kf / hdt:.0f} frames/s, load {hash_res['load_factor']}, "
             f"pool {info['pool_capacity']} blocks for {info['used']} live")
         ht.close()

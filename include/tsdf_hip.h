@@ -75,6 +75,9 @@ typedef struct {
                                  after a synchronous call; see tsdf_hash_integrate_batch) */
     int64_t list_errors;      /* brick-list entries out of range, dropped by the integrate kernel
                                  (always 0 unless device memory was corrupted) */
+    int64_t batch_voxels;     /* sum over launches of U_batch: the voxels updated at least once by
+                                 the launch's temporal batch (<= voxel_updates; each such voxel's
+                                 state is read and written once per launch -- the roofline's bytes) */
 } tsdf_stats_t;
 
 typedef struct {

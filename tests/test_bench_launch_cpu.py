@@ -54,3 +54,17 @@ def test_rccl_without_enough_gpus_fails_loudly():
     assert r.returncode != 0
     assert not _json_lines(r.stdout)
     assert "needs 2 GPUs" in r.stderr
+
+
+def test_launcher_without_gpus_takes_its_world_size():
+    """(round-4 advisor) `torchrun --nproc-per-node N bench.py` without --gpus runs N ranks."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", f"--master-port={port}", BENCH, "--dist-backend", "gloo",
+                        "--launch-selftest"], capture_output=True, text=True, timeout=180, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert _json_lines(r.stdout)[0]["n_gpus"] == 2

@@ -22,8 +22,8 @@ def bench(monkeypatch):
 
 
 def _roof():
-    return {"bound": "hbm", "achieved": 9000.0, "peak": 8000.0, "frac": 1.125, "kernel_avg_us": 650.0,
-            "bytes_per_launch": 6.0e9, "launches": 20}
+    return {"bound": "hbm", "achieved": 3000.0, "peak": 8000.0, "frac": 0.375, "kernel_avg_us": 650.0,
+            "bytes_per_launch": 1.95e9, "launches": 20}
 
 
 def _profiles(tmp_path, build, workload):
@@ -38,23 +38,46 @@ def _profiles(tmp_path, build, workload):
 def test_profiles_attach_only_for_the_same_build_and_workload(bench, tmp_path, monkeypatch):
     st = {"voxel_updates": 20 * 16 * 15_000_000, "kernel_launches": 20}
     pmc, sq = _profiles(tmp_path, "abc", bench.WORKLOAD)
-    monkeypatch.setattr(bench, "PMC_PROFILE", pmc)
-    monkeypatch.setattr(bench, "SQ_PROFILE", sq)
     roof = _roof()
-    bench.attach_profiles(roof, st, "abc")
+    bench.attach_profiles(roof, st, "abc", pmc, sq, bench.WORKLOAD)
     assert roof["traffic"] == 2_200_000_000 and roof["bound"] == "valu"
+    assert roof["traffic_over_algorithmic"] == pytest.approx(2.2e9 / 1.95e9, abs=1e-3)
     assert roof["traffic_frac"] == pytest.approx(2.2e9 / 650e-6 / 8e12, abs=1e-4)
     assert roof["valu"]["valu_busy"] == 0.88 and "profiles_note" not in roof
     roof = _roof()
-    bench.attach_profiles(roof, st, "other")  # another build: nothing attached, and said why
+    bench.attach_profiles(roof, st, "other", pmc, sq, bench.WORKLOAD)  # another build: nothing attached, and said why
     assert "traffic" not in roof and "valu" not in roof and roof["bound"] == "hbm"
     assert "measured library build abc, this is other" in roof["profiles_note"]
     pmc, sq = _profiles(tmp_path, "abc", "another workload")
-    monkeypatch.setattr(bench, "PMC_PROFILE", pmc)
-    monkeypatch.setattr(bench, "SQ_PROFILE", sq)
     roof = _roof()
-    bench.attach_profiles(roof, st, "abc")
+    bench.attach_profiles(roof, st, "abc", pmc, sq, bench.WORKLOAD)
     assert "traffic" not in roof and "measured another workload" in roof["profiles_note"]
+
+
+def test_roofline_prices_each_batched_voxel_once(bench):
+    """temporal batching must never push roofline.achieved past peak.  A launch of 16
+    frames whose batch updates U distinct voxels moves 24 B of state per distinct voxel, however
+    many of its frames update each one: the frac follows U, and the per-frame pricing (24 B per
+    update) is only a named secondary figure."""
+    L, F = 20, 320
+    st = {"voxel_updates": F * 15_700_000, "batch_voxels": L * 80_000_000, "kernel_launches": L,
+          "kernel_ms": L * 0.652}
+    r = bench.integrate_roofline(st, F, "k")
+    alg = 24.0 * L * 80_000_000 + 5.0 * bench.PIX * F
+    assert r["bytes_per_launch"] == round(alg / L)
+    assert r["frac"] == pytest.approx(alg / (L * 0.652e-3) / 8e12, abs=1e-4) and r["frac"] < 1
+    assert r["per_frame_bytes_frac"] > 1 > r["frac"]  # what round 4's line reported as frac
+    h = bench.integrate_roofline(st, F, "k", blocks_touched=1000)
+    assert h["bytes_per_launch"] == round((alg + 16.0 * 1000) / L)
+    assert bench.integrate_roofline(dict(st, kernel_launches=0), F, "k") is None
+
+
+def test_bound_names_the_resource_closest_to_its_peak(bench, tmp_path):
+    st = {"voxel_updates": 20 * 16 * 15_000_000, "kernel_launches": 20}
+    pmc, sq = _profiles(tmp_path, "abc", bench.WORKLOAD)
+    roof = dict(_roof(), frac=0.95)  # memory nearer its peak than the VALU's 0.88
+    bench.attach_profiles(roof, st, "abc", pmc, sq, bench.WORKLOAD)
+    assert roof["bound"] == "hbm" and "bound_note" not in roof
 
 
 def _pmc_csv(path, values, kernel):

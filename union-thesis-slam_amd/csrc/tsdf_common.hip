@@ -589,6 +589,7 @@ int Base::read_stats(tsdf_stats_t* out, int reset) {
     out->kernel_launches = prof.launches;
     out->bricks_skipped = (int64_t)s[ST_OVERFLOW];
     out->list_errors = (int64_t)s[ST_BAD_ENTRY];
+    out->batch_voxels = (int64_t)s[ST_UNIQUE];
     if (reset) {
         TSDF_HIP(hipMemsetAsync(stats, 0, sizeof(unsigned long long) * h.size(), stream));
         TSDF_HIP(hipStreamSynchronize(stream));

@@ -26,8 +26,10 @@ constexpr int kStatSpread = 64;     // counters are spread over 64 words (no hot
 constexpr unsigned long long kEmpty = ~0ull;
 constexpr unsigned long long kTomb = ~0ull - 1ull;
 
+// ST_UNIQUE: voxels updated at least once by a launch's batch (each voxel's state is read and
+// written once per batch however many of its frames update it: the roofline's state bytes)
 enum Stat { ST_VOXELS = 0, ST_VISITED, ST_TOUCHED, ST_ALLOC, ST_PROBE, ST_LOOKUPS, ST_OVERFLOW,
-            ST_PROBE_MAX, ST_BAD_ENTRY, kNStat };
+            ST_PROBE_MAX, ST_BAD_ENTRY, ST_UNIQUE, kNStat };
 
 // Volume geometry (by value in kernel arguments -> scalar registers).
 struct Vol {
@@ -709,9 +711,10 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, ListEntry entry, int zoff,
                                        unsigned long long* s_stat, const double* s_rcp,
-                                       unsigned& nupd, int* res = nullptr) {
+                                       unsigned& nupd, unsigned& nuniq, int* res = nullptr) {
     // nupd: the wave's voxel updates, accumulated over its items (scalar popcounts of the step
-    // masks; integrate_list adds it to the statistics once per wave)
+    // masks; integrate_list adds it to the statistics once per wave); nuniq: the voxels among them
+    // updated at least once in the batch (popcounts of the OR of each step's masks over the frames)
     static_assert(NZ == 8 || NZ == 4, "z-parts of 8 or 4 steps");
     constexpr bool kHalfHash = HASH && NZ == 4;  // (requires res)
     const int lane = lane_id();
@@ -813,9 +816,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     bool loaded[kH];
 #pragma unroll
     for (int h = 0; h < kH; ++h) loaded[h] = kHalfHash && blk < 0;  // a missing hash block: fresh state
-    // voxels updated by any frame of the batch (entry bits, hash): per z-step, the OR of the
-    // step masks' ballots -- scalar registers and scalar ORs, no per-lane VGPR bit field
-    unsigned long long touched[HASH ? NZ : 1] = {};
+    // voxels updated by any frame of the batch (entry bits of the hash, ST_UNIQUE): per z-step,
+    // the OR of the step masks' ballots -- scalar registers and scalar ORs, no per-lane VGPR bit field
+    unsigned long long touched[NZ] = {};
     bool w_small = true;   // all loaded weights are integers that stay < kRcpTab in this batch
     bool w_table = true;   // ... < kRcpBig
     bool c_canon = true;   // all loaded colours are canonical (canon_color)
@@ -913,12 +916,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }
 #pragma unroll
         for (int h = 0; h < kH; ++h) loaded[h] |= need[h];
-        if constexpr (HASH) {
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) touched[k] |= __ballot(okv[k]);
+        for (int k = 0; k < NZ; ++k) {
+            const unsigned long long m = __ballot(okv[k]);
+            touched[k] |= m;
+            nupd += (unsigned)__popcll(m);  // (wave total, scalar)
         }
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) nupd += (unsigned)__popcll(__ballot(okv[k]));  // (wave total, scalar)
         // phase 5: update in registers, straight-line; invalid steps keep their old values.
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
@@ -1095,6 +1098,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         return;  // no frame of the batch updated this brick
     }
 
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) nuniq += (unsigned)__popcll(touched[k]);
     // phase 6: store the changed halves once (a new hash block is written whole: its init)
     const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
 #pragma unroll
@@ -1324,29 +1329,34 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                       unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd);
+                                       unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
+                                       unsigned& nuniq);
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                       unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
-    unsigned nupd = 0;  // the wave's voxel updates over all its items (ST_VOXELS; wave-uniform)
+    unsigned nupd = 0, nuniq = 0;  // the wave's voxel updates over all its items (ST_VOXELS, ST_UNIQUE; wave-uniform)
     integrate_items<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
-                                           s_next, wg, n_wg, res, nupd);
-    if (lane_id() == 0 && nupd) atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
+                                           s_next, wg, n_wg, res, nupd, nuniq);
+    if (lane_id() == 0 && nupd) {
+        atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
+        atomicAdd(&s_stat[ST_UNIQUE], (unsigned long long)nuniq);
+    }
 }
 
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                       unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd) {
+                                       unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
+                                       unsigned& nuniq) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
             integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[e / parts], (e % parts) * NZ,
-                                                   s_stat, s_rcp, nupd);
+                                                   s_stat, s_rcp, nupd, nuniq);
         return;
     }
     // k_cull's list: one sub-list per cost class (frames kept, 1..kMaxBatch), taken most frames
@@ -1427,14 +1437,14 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             int zn = 0;
             const bool more = take(en, zn);
             // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, res);
+            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
             have = more;
             e = en;
             zoff = zn;
         }
 #else
         while (take(e, zoff))  // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, res);
+            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
 #endif
         if (use_prio) __builtin_amdgcn_s_setprio(0);
         return;
@@ -1447,7 +1457,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             nc = min(coh_load(&count[c + 1]), nbk);
         }
         integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
-                                               (e % parts) * NZ, s_stat, s_rcp, nupd, res);
+                                               (e % parts) * NZ, s_stat, s_rcp, nupd, nuniq, res);
     }
 }
 

@@ -42,7 +42,8 @@ class Stats(ctypes.Structure):
                 ("blocks_allocated", ctypes.c_int64), ("probe_steps", ctypes.c_int64),
                 ("probe_max", ctypes.c_int64), ("lookups", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
-                ("bricks_skipped", ctypes.c_int64), ("list_errors", ctypes.c_int64)]
+                ("bricks_skipped", ctypes.c_int64), ("list_errors", ctypes.c_int64),
+                ("batch_voxels", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
