@@ -78,9 +78,12 @@ def test_async_hash_overflow_is_reported_not_replayed(monkeypatch):
     """A pool far too small for asynchronous launches: the skipped bricks cannot be re-run (their
     frames are gone), so the library reports TSDF_E_CAPACITY once, clears the overflow list (no
     later call replays it against other frames), and the handle works again after reset().  (The
-    copy-grown pool: a mapped pool grows in 32 MB pieces, which hold this whole extent.)"""
+    copy-grown pool: a mapped pool grows in 32 MB pieces, which hold this whole extent; and no
+    growth ahead of the asynchronous launches, TSDF_HASH_ASYNC_GROW=0, which would otherwise keep
+    room for them.)"""
     from tsdf_amd import _ffi, grid_fusion, hash_fusion
     monkeypatch.setenv("TSDF_HASH_VMM", "0")
+    monkeypatch.setenv("TSDF_HASH_ASYNC_GROW", "0")
     d, c, poses = _synth(24, start=700)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     Tinv = np.linalg.inv(poses)

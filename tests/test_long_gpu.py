@@ -7,9 +7,10 @@
     table and the 65519 limit of the whole table (kRcpTab / kRcpBig less kMaxBatch + 1 = 17,
     csrc/tsdf_device.h; the preloaded ranges also straddle 4087 / 65527 of -DTSDF_MAX_BATCH=8) and
     non-canonical colours, preloaded with set_state;
-  * config[4] per rank: bucket-range hash shard 5 of 8 over a 1024^3 @ 1 cm extent with 2^22
-    buckets over 500 frames, against dense slabs (and the oracle) on rows restricted to the
-    shard's blocks;
+  * config[4] per rank: bucket-range hash shard 5 of 8 over a 1024^3 @ 1 cm extent over its whole
+    10,000-frame sequence in one asynchronous call (the table doubles under the 0.75 policy and
+    the pool grows mid-run), against dense slabs (and those against the oracle) on rows restricted
+    to the shard's blocks;
   * the hash's f32 state against the reference's float64 Voxel (voxel.py:19-49) over 500 frames,
     within north_star's 1e-4.
 """
@@ -74,18 +75,13 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
 
 
 @pytest.mark.timeout(400)
-def test_config3_rank_shard_10000_frames_full_sequence():
-    """config[3]'s whole sequence on one rank (BASELINE: 10k frames; the demo loop is
-    grid_demo1.py:76-87): cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 10,000 frames of
-    the bench trajectory (625 16-frame batches through the pipelined launches).  Weights pass the 4079
-    limit of the LDS part of the reciprocal table by accumulation alone (no preload), so waves
-    move to the HBM table mid-run, and stay below the whole table's 65519.  The two rows holding
-    the largest weights equal the oracle bit for bit; the frames stay in HBM (15 GB) and reach
-    the host in chunks for the oracle."""
+@pytest.fixture(scope="module")
+def bench10k():
+    """The bench trajectory's first 10,000 frames in HBM (15 GB: u16 depth bits as int16, RGB8),
+    shared by the 10k-frame tests of config[3] and config[4]."""
     import torch
-    from tsdf_amd import grid_fusion, scene, sharding
-    n, chunk = 10000, 1000
-    K = scene.intrinsics()
+    from tsdf_amd import scene
+    n = 10000
     dev = torch.device("cuda", 0)
     poses = scene.trajectory(n, seed=0, radius_frac=scene.BENCH_RING)
     spheres = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
@@ -96,6 +92,23 @@ def test_config3_rank_shard_10000_frames_full_sequence():
         depth[s:s + len(d)] = d
         rgb[s:s + len(c)] = c
     torch.cuda.synchronize()
+    yield depth, rgb, poses
+    del depth, rgb
+    torch.cuda.empty_cache()
+
+
+def test_config3_rank_shard_10000_frames_full_sequence(bench10k):
+    """config[3]'s whole sequence on one rank (BASELINE: 10k frames; the demo loop is
+    grid_demo1.py:76-87): cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 10,000 frames of
+    the bench trajectory (625 16-frame batches through the pipelined launches).  Weights pass the 4079
+    limit of the LDS part of the reciprocal table by accumulation alone (no preload), so waves
+    move to the HBM table mid-run, and stay below the whole table's 65519.  The two rows holding
+    the largest weights equal the oracle bit for bit; the frames stay in HBM (15 GB) and reach
+    the host in chunks for the oracle."""
+    from tsdf_amd import grid_fusion, scene, sharding
+    depth, rgb, poses = bench10k
+    n, chunk = len(poses), 1000
+    K = scene.intrinsics()
     Tinv = np.linalg.inv(poses)
     bnds = np.array([[0.0, ROOM]] * 3)
     vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(3, 8))
@@ -158,33 +171,43 @@ def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched, w_lo
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
 
 
-def test_config4_rank_hash_shard_1024_extent():
-    """One rank of config[4]: bucket-range shard 5 of 8 over a 1024^3 @ 1 cm extent (2^21 bricks,
-    21-bit key fields up to 127), 2^22 buckets, 500 frames.  On three x rows: a voxel is found iff
-    its block's home bucket is in the shard's range and the dense grid updated it, with the dense
-    grid's exact values; the dense rows equal the oracle."""
+def test_config4_rank_hash_shard_1024_extent_10000_frames(bench10k):
+    """config[4]'s whole per-rank sequence (BASELINE: 10k frames, bucket-range sharded, 1024^3 @
+    1 cm; the reference loop is hash_demo1.py:114-125): shard 5 of 8 of a table created with 2^17
+    slots (so the reference's 0.75 load-factor policy doubles it mid-run) and a pool of 2^14 blocks
+    (grown ahead of the launches in flight), integrating 10,000 bench frames in one asynchronous
+    call.  No brick is skipped, the table doubled, and on two x rows a voxel is found iff its
+    block's home bucket (in the table size of create) is in the shard's range and the dense grid
+    updated it, with the dense grid's exact values; the dense rows equal the oracle bit for bit."""
     from tsdf_amd import grid_fusion, hash_fusion, scene, sharding
-    n = 500
-    depth, rgb, poses = _frames_on_device(n, start=300)
+    depth, rgb, poses = bench10k
+    n, chunk = len(poses), 1000
     K = scene.intrinsics()
     Tinv = np.linalg.inv(poses)
     bnds = np.array([[0.0, ROOM]] * 3)
-    ht = hash_fusion.HashTable(bnds.copy(), 0.01, 1 << 22, shard=5, n_shards=8, max_blocks=1 << 16)
+    ht = hash_fusion.HashTable(bnds.copy(), 0.01, 1 << 17, shard=5, n_shards=8, max_blocks=1 << 14)
     assert tuple(int(x) for x in ht._vol_dim) == (1024, 1024, 1024)
-    ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True)
-    rows = [100, 517, 1023]
-    dh, ch = depth.cpu().numpy().view(np.uint16), rgb.cpu().numpy()
+    ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=False)
+    ht.sync()  # (raises TSDF_E_CAPACITY if an asynchronous launch skipped a brick)
+    info = ht.info()
+    assert ht.stats()["bricks_skipped"] == 0 and ht.stats()["list_errors"] == 0
+    assert info["capacity"] > 1 << 17 and info["used"] > 100_000 and info["pool_capacity"] > 1 << 14
+    rows = [300, 700]
     orc = O.OracleTSDFVolume(bnds.copy(), 0.01, x_index=np.array(rows))
-    for f in range(n):
-        orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[f])
+    slabs = [grid_fusion.TSDFVolume(bnds.copy(), 0.01, slab=(x, x + 1)) for x in rows]
+    for sl in slabs:
+        sl.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=False)
+    for c0 in range(0, n, chunk):
+        dh = depth[c0:c0 + chunk].cpu().numpy().view(np.uint16)
+        ch = rgb[c0:c0 + chunk].cpu().numpy()
+        for f in range(len(dh)):
+            orc.integrate(ch[f], dh[f].astype(float) / 1000.0, K, poses[c0 + f])
     yy, zz = np.meshgrid(np.arange(1024), np.arange(1024), indexing="ij")
     n_found = n_upd = 0
-    for i, x in enumerate(rows):
-        sl = grid_fusion.TSDFVolume(bnds.copy(), 0.01, slab=(x, x + 1))
-        sl.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True)
+    for i, (x, sl) in enumerate(zip(rows, slabs)):
         T, W, C = (a[0] for a in sl.get_state())
         assert _same(T, orc._tsdf_vol_cpu[i]) and _same(W, orc._weight_vol_cpu[i]) and _same(C, orc._color_vol_cpu[i])
-        own = sharding.hash_owner(x // 8, yy // 8, zz // 8, 1 << 22, 8) == 5
+        own = sharding.hash_owner(x // 8, yy // 8, zz // 8, 1 << 17, 8) == 5
         ijk = np.stack([np.full(yy.size, x), yy.reshape(-1), zz.reshape(-1)], 1)
         found, t, w, c = ht.lookup(ijk)
         found = found.reshape(1024, 1024)
@@ -194,8 +217,6 @@ def test_config4_rank_hash_shard_1024_extent():
         m = found.reshape(-1)
         assert _same(t[m], T.reshape(-1)[m]) and _same(w[m], W.reshape(-1)[m]) and _same(c[m], C.reshape(-1)[m])
     assert 0 < n_found < n_upd
-    info = ht.info()
-    assert info["used"] > 10_000 and ht.stats()["list_errors"] == 0
 
 
 def test_hash_f32_state_within_1e4_of_reference_f64_voxels_over_500_frames():

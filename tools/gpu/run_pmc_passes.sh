@@ -1,5 +1,6 @@
 # The two PMC traffic passes (FETCH_SIZE, WRITE_SIZE; --kernel-trace only beside --pmc) and the SQ
-# pass, each a dense-only bench at the driver's window (--steps 20 --warmup 5).
+# pass, each the bench's dense and hash legs at the driver's window (--steps 20 --warmup 5): the
+# counters of both integrate launches (k_fused, k_fused_hash) come from the same passes.
 set -o pipefail
 R=$(pwd)
 O="$R/gpurun_out/profile"
@@ -8,8 +9,8 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for pass in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/pmc_$i -o pmc -- python "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-hash --no-cpu --no-profile --no-ingest --no-dropin --no-mesh --no-lounge > "$O/pmc_$pass.json" 2> "$O/pmc_$pass.err" || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/pmc_$i -o pmc -- python "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu --no-profile --no-ingest --no-dropin --no-mesh --no-lounge > "$O/pmc_$pass.json" 2> "$O/pmc_$pass.err" || exit $?
   f=$(find /tmp/pmc_$i -name "*counter_collection.csv" | head -1)
-  [ -n "$f" ] && grep -E "tsdf|Counter_Name" "$f" > "$O/pmc_$pass.csv"
+  [ -n "$f" ] && grep -E "k_fused|Counter_Name" "$f" > "$O/pmc_$pass.csv"
 done
 cd "$R" && bash tools/gpu/run_pmc_sq.sh

@@ -8,6 +8,9 @@ bench line printed under the profiler):
                                        average (must agree with the line's roofline.kernel_avg_us)
   profiles/pmc_integrate_<tag>.json    HBM traffic per timed integrate launch (FETCH_SIZE/WRITE_SIZE)
   profiles/pmc_sq_<tag>.json           SQ issue counters per timed integrate launch
+  profiles/pmc_hash_<tag>.json         the same counters (traffic + SQ) of the hash launch
+                                       k_fused_hash<0> in the bench's inserting hash window (and,
+                                       as a second block, in its no-allocation repeat window)
 
 The timed launches: every bench.py call of n batches issues n + 2 pipelined launches of
 k_fused<true, 4, 0> (the cold window, the clock warm-up, the W warm-up steps, then the timed call,
@@ -150,8 +153,65 @@ def sq(tag):
     print(json.dumps(out, indent=1))
 
 
+HASH_KERNEL = "k_fused_hash<0>"
+SQ_NAMES = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+            "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+
+
+def hash_windows(path):
+    """Per-dispatch counters of k_fused_hash<0> in one pass -> (inserting window, repeat window):
+    the hash leg ends with the timed call (K + 2 launches: two pipeline fills, then K integrating)
+    and the no-allocation repeat (K + 2 more), the process's last 2 (K + 2) launches of the kernel."""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if HASH_KERNEL not in r["Kernel_Name"]:
+            continue
+        d = per.setdefault(int(r["Dispatch_Id"]), {})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    rows = [per[k] for k in sorted(per)][-2 * (K + 2):]
+    if len(rows) != 2 * (K + 2):
+        raise RuntimeError(f"{path}: {len(rows)} hash launches, expected {2 * (K + 2)}")
+    return rows[2:K + 2], rows[K + 4:]
+
+
+def hash_profile(tag):
+    """profile/pmc_{FETCH,WRITE}_SIZE.csv and pmc_sq/pmc_sq.csv -> profiles/pmc_hash_<tag>.json."""
+    src = os.path.join(REPO, "gpurun_out", "profile")
+    sys.path.insert(0, REPO)
+    import bench
+    out = {"kernel": "tsdf::" + HASH_KERNEL, "workload": bench.HASH_WORKLOAD,
+           "window": f"bench.py --gpus 1 --steps {K} --warmup {W}, hash leg: the {K} timed launches of the "
+                     "inserting window (median); no_alloc_repeat: the same window again"}
+    blocks = {"inserting": {}, "no_alloc_repeat": {}}
+    for path, names in ((os.path.join(src, "pmc_FETCH_SIZE.csv"), ["FETCH_SIZE"]),
+                        (os.path.join(src, "pmc_WRITE_SIZE.csv"), ["WRITE_SIZE"]),
+                        (os.path.join(REPO, "gpurun_out", "pmc_sq", "pmc_sq.csv"), SQ_NAMES)):
+        ins, rep = hash_windows(path)
+        for key, rows in (("inserting", ins), ("no_alloc_repeat", rep)):
+            for n in names:
+                blocks[key][n] = statistics.median(r[n] for r in rows)
+    for key, m in blocks.items():
+        m["hbm_bytes"] = round(1024 * (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]))
+        m["valu_busy_per_simd"] = round(m["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * m["GRBM_GUI_ACTIVE"] / 8), 3)
+        m["wait_any_frac"] = round(m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"], 3)
+    ins = blocks["inserting"]
+    out["build_id"] = bench_line(os.path.join(src, "pmc_FETCH_SIZE.json")).get("build_id")
+    out["hbm_bytes_per_launch"] = ins["hbm_bytes"]
+    out["median_per_launch"] = {n: ins[n] for n in SQ_NAMES}
+    out["valu_busy_per_simd"] = ins["valu_busy_per_simd"]
+    out["wait_any_frac"] = ins["wait_any_frac"]
+    out["no_alloc_repeat"] = blocks["no_alloc_repeat"]
+    out["note"] = ("FETCH_SIZE doubled per the gfx950 rule (as pmc_integrate_*); SQ cycle counters in quad-cycles; "
+                   "busy = ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")
+    with open(os.path.join(REPO, "profiles", f"pmc_hash_{tag}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "sq":
         sq(*sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "hash":
+        hash_profile(*sys.argv[2:])
     else:
         main(*sys.argv[1:])

@@ -405,24 +405,22 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->fy = (double)(float)K[4];
         fr->cx = (double)(float)K[2];
         fr->cy = (double)(float)K[5];
-        const double margin = frame_margin(W, H, fr->cx, fr->cy);
-        fr->half_m = 0.5 - margin;
         for (int j = 0; j < 4; ++j) {
             fr->Tf[j] = T[j] * fr->fx;
             fr->Tf[4 + j] = T[4 + j] * fr->fy;
         }
-        {  // the fast path's depth limit (fold_bound) as the high dword of a positive f64, rounded up
-            double wmax[3];
+        {  // the certified f32 filter's constants (csrc/tsdf_device.h, f32_filter_consts): the
+           // volume's world box (global voxel indices of this shard's extent) and coordinate bounds
+            double lo[3], hi[3], wmax[3];
             for (int a = 0; a < 3; ++a) {
-                const long long gmax = (a == 0 ? (long long)vol.off[0] + col_gx(vol, vol.nb[0] - 1) + kBrickEdge
-                                               : (long long)vol.off[a] + vol.dims[a]);
-                wmax[a] = fabs((double)vol.origin[a]) + vol.vs * (double)gmax + 1.0;
+                const long long g0 = (long long)vol.off[a];
+                const long long g1 = (a == 0 ? (long long)vol.off[0] + col_gx(vol, vol.nb[0] - 1) + kBrickEdge - 1
+                                             : (long long)vol.off[a] + vol.dims[a] - 1);
+                lo[a] = (double)vol.origin[a] + vol.vs * (double)g0;
+                hi[a] = (double)vol.origin[a] + vol.vs * (double)g1;
+                wmax[a] = fmax(fabs(lo[a]), fabs(hi[a])) + vol.vs + 1.0;
             }
-            const double zmin = fold_bound(T, fr->fx, fr->fy, wmax, margin);
-            long long bits;
-            std::memcpy(&bits, &zmin, sizeof bits);
-            const long long hi = (std::isfinite(zmin) && zmin < 1e300) ? (bits >> 32) + 1 : 0x7FEFFFFFll;
-            fr->zmin_hi = (int)std::min<long long>(hi, 0x7FEFFFFFll);
+            f32_filter_consts(&fr->ff, T, fr->Tf, fr->fx, fr->fy, fr->cx, fr->cy, W, H, lo, hi, wmax, vol.vs, vol.trunc);
         }
         fr->ow = ow ? ow[first + i] : ow_default;
         fr->ow32 = (float)fr->ow;

@@ -559,3 +559,14 @@ extern "C" int tsdf_diag_wg_times(unsigned long long* out) {
     return TSDF_OK;
 }
 #endif
+
+#ifdef TSDF_DIAG
+// (diagnostic builds) the integrate's path counters (g_ddiag, csrc/tsdf_device.h), read and cleared
+extern "C" int tsdf_diag_counts(unsigned long long* out) {
+    TSDF_HIP(hipDeviceSynchronize());
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(tsdf::g_ddiag), sizeof(unsigned long long) * 8));
+    const unsigned long long zero[8] = {};
+    TSDF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(tsdf::g_ddiag), zero, sizeof(zero)));
+    return TSDF_OK;
+}
+#endif

@@ -16,6 +16,8 @@
 #include <stdint.h>
 #include <type_traits>
 
+#include "tsdf_filter.h"
+
 namespace tsdf {
 
 constexpr int kBrickEdge = 8;
@@ -61,9 +63,12 @@ struct Frame {
     double T[12];             // rows 0..2 of inv(cam_pose), row-major
     double fx, fy, cx, cy;    // f64(f32(K))  (cam2pix casts intr to float32, grid_fusion.py:190)
     double ow;                // obs_weight as a Python float (f64)
-    double half_m;            // 0.5 - the fast pixel path's boundary margin (frame_margin)
-    double Tf[8];             // the fast pixel path's rows: RN(T[0..3] * fx), RN(T[4..7] * fy)
-    int zmin_hi;              // ... and its depth limit: high dword of zmin (fold_bound, host)
+    double Tf[8];             // the f32 filter's x / y rows: RN(T[0..3] * fx), RN(T[4..7] * fy)
+    // The certified f32 filter (project_part; host: f32_filter_consts): per step,
+    // camera z and the pixel numerators in f32 from the part's first step, Z_k = Z0 + Tz32 * dz_k,
+    // X_k = X0 + Tx32 * dz_k, Y_k = Y0 + Ty32 * dz_k, and s = X_k * rcp(Z_k) + (cx + 0.5).  Every
+    // decision is taken in f32 only where its error bound makes it certain; the rest is redone in f64.
+    F32Filter ff;
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
     const void* depth;        // depth read by cull/integrate: u16 millimetres or f64 metres
@@ -104,9 +109,6 @@ static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
 #endif
 constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxBatch;
 // integrate_items / integrate_brick options (A/B builds)
-#ifndef TSDF_OCC_RMW  // hash z-half waves: entry words read at item start, stored if changed
-#define TSDF_OCC_RMW 0
-#endif
 #ifndef TSDF_XCD_DEAL  // deal list items to workgroups XCD by XCD (integrate_items): dense -1.5 %,
 #define TSDF_XCD_DEAL 1  // hash -1 % per launch, hash eighth shard +3 % (profiles/r04_i/)
 #endif
@@ -114,12 +116,10 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_RES_PREFETCH  // hash: read the claim word with the item's first instructions
-#define TSDF_RES_PREFETCH 0
-#endif
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
-// (1..kMaxBatch); word kDoneWord = integrate workgroups finished (fused hash launch).
-constexpr int kCountWords = 32, kDoneWord = 24;
+// (1..kMaxBatch); words kDoneWord / kDoneWordC = integrate and cull workgroups finished (fused hash
+// launch; the launch counts on its cull's set, or on its integrate's set when it has no cull).
+constexpr int kCountWords = 32, kDoneWord = 24, kDoneWordC = 25;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 // The whole table in HBM (512 KB, L2-resident) for waves with a weight past the LDS part (long
 // runs: weights pass 4079 after ~4300 frames of a room seen from inside); 65536 keeps every colour
@@ -160,6 +160,7 @@ struct PoolState {
     long long cursor;      // allocations made by the current launch
     long long n_overflow;  // bricks skipped for lack of space (re-run after growing)
     long long tombs;       // keys tombstoned since the table was last rebuilt (>= tombstones in it)
+    long long n_inserted;  // blocks the fused launches' culls inserted since the last k_free_unused
 };
 
 // Pool state after launch `seq`, written by the committing thread into page-locked host memory
@@ -169,7 +170,8 @@ struct PoolState {
 constexpr int kReports = 8;
 struct PoolReport {
     long long pool_top, free_count, n_overflow;
-    long long listed;  // bricks the launch's cull listed: a bound on the blocks one batch can allocate
+    long long listed;  // bricks the launch's cull listed: a bound on the blocks one launch can allocate
+    long long tombs;   // PoolState::tombs
     long long seq;     // launch number + 1 (0: slot never written)
 };
 
@@ -186,6 +188,8 @@ struct Table {
     long long max_blocks;
     const int* owned;           // bucket-range shards: the bricks this shard owns, increasing (else null)
     int n_owned;
+    int* ins_list;              // fused launches: bricks their culls inserted (k_free_unused; ins_cap)
+    long long ins_cap;
     int overflow_cap;
     int int_bits;               // 64: NumPy int64; 32: wrapping int32 (author's Windows run)
 };
@@ -467,13 +471,6 @@ __device__ inline double depth_m(const FrameBufs& fb, unsigned p, unsigned raw) 
     return buf_ld_f64(fb.depth, (int)p, 0, 0, 0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Reciprocal of z for the fast pixel path: the bare v_rcp_f64, accurate to 2^-24.4 relative
-// (random z in [1e-3, 1e3] and a 2^28-point mantissa sweep: tools/gpu/rcp_probe.hip), so
-// u = (x*fx)*rz + cx lies within |u - cx| * 2^-24.3 of the reference's (x*fx)/z + cx (< 3e-5 px
-// for 640x480).  Steps whose u is within frame_margin of a rounding boundary (or not finite) are recomputed with the reference's own division (a Newton-refined reciprocal
-// with a 1e-9 px margin ran 2.6 % slower: the two FMAs cost more than the extra slow steps).
-// ---------------------------------------------------------------------------------------------
 // RN(a / b) given y = RN(1 / b): Markstein's correction step.  q0 = RN(a*y) is within 1 ulp
 // of a/b, r = a - b*q0 is exact with an FMA, and RN(q0 + r*y) is then the correctly rounded
 // quotient (Markstein 1990; Muller et al., Handbook of Floating-Point Arithmetic, "Markstein's
@@ -502,29 +499,34 @@ __device__ inline f2 div_rn32x2(f2 a, f2 b, f2 y) {  // div_rn32 on both lanes
     return pk_fma(r, y, q0);
 }
 
-// The fast path's pixel error is < |u - c| * 2^-24.3 (the bare reciprocal), and wherever the
-// boundary test matters |u - c| <= max(W, H) + max(|cx|, |cy|) -- a step closer than this margin to
-// a rounding boundary takes the exact path.  1e-4 px covers images up to ~1000 px; larger ones
-// scale it.  Host-side: stored per frame as half_m = 0.5 - margin.
-inline double frame_margin(int W, int H, double cx, double cy) {
-    const double span = (double)(W > H ? W : H) + fmax(fabs(cx), fabs(cy));
-    return fmax(1e-4, 1e-7 * span);
-}
-
-// The fast path folds fx, fy and the translation into its rows: X = fma(Tf2, pz, fma(Tf1, py,
-// fma(Tf0, px, Tf3))) with Tf = RN(T * f) -- four roundings, each within 2^-53 of its operands'
-// magnitudes, so |X - f * x| <= E = 8 * 2^-53 * f * (|T0| X + |T1| Y + |T2| Z + |T3|) for world
-// coordinates bounded by (X, Y, Z) (a factor 2 of slack).  Its pixel error E / z stays below a
-// quarter of the margin where z > zmin = 4 E / margin.  Returns zmin (host).
-inline double fold_bound(const double* T, double fx, double fy, const double wmax[3], double margin) {
-    double e = 0.0;
-    for (int r = 0; r < 2; ++r) {
-        const double* t = T + 4 * r;
-        const double s = fabs(t[0]) * wmax[0] + fabs(t[1]) * wmax[1] + fabs(t[2]) * wmax[2] + fabs(t[3]);
-        e = fmax(e, 8.0 * 0x1p-53 * (r == 0 ? fx : fy) * s);
-    }
-    return 4.0 * e / margin;
-}
+// ---------------------------------------------------------------------------------------------
+// The certified f32 filter (round 5).  The reference projects every voxel in f64 (SURVEY §8(a)
+// a4-a6): z, then u = rint((x*fx)/z + cx), v likewise, and tests z > 0, the bounds, depth > 0,
+// depth - z >= -trunc.  Of those f64 values the result needs exactly only the decisions and, for
+// voxels in the truncation band, depth - z itself (dist = min(1, (depth - z) / trunc) is 1 exactly
+// wherever depth - z >= trunc, i.e. in free space).  So every step is first classified in f32 --
+// camera z and the pixel numerators stepped from the part's first step, one v_rcp_f32, packed
+// arithmetic two steps per instruction -- and a decision is taken there only where the f32 error
+// bound below makes it certain; a pixel coordinate within the margin of a rounding boundary (or z
+// below zmin) is redone with the reference's f64 division, and a step in the band (or near either
+// truncation limit) gets its exact f64 z, depth and difference.  Results are bit-identical to the
+// f64 path: the f32 values only ever choose between outcomes that the bound proves equal.
+//
+// Error bound (host, f32_filter_consts), per pixel axis with focal f, centre c, image side N, for a
+// step with z >= zmin whose pixel is within a pixel of the image (q = max(|c|, |N - c|) + 1.5 bounds
+// |X / Z|; farther pixels are out of bounds whichever way they round):
+//   X0 = RN32(X(pz0)) (f64 chain, then one rounding), X_k = RN32(Tx32 * dz_k + X0): |X_k - X| <=
+//   2^-24 (2|X| + 2|Tx| dz) with dz <= (steps - 1) * vs; Z likewise with |Tz|; rcp_f32 <= 1 ulp;
+//   s = RN32(X_k * r + RN32(c + 0.5)) adds 2^-24 (q + 1.5 (|c| + 0.5)).  So
+//     |s - (X / Z + c + 0.5)| <= 1.01 * 2^-24 (7 q + 1.5 (|c| + 0.5) + 2 dz (|Tx| + q |Tz|) / zmin)
+//   plus the f64 folding error of X0 (fold_error / zmin).  The margin is 1.1 x that; zmin keeps the
+//   dz term at half the rest (640x480, 2 cm voxels: margin 2.8e-4 px, zmin 0.08 m for 4-step parts).
+//   depth - z: |d32 - d| <= 1.8 * 2^-24 d (u16 * 0.001f), |Z_k - z| <= 2^-24 (2 |z| + 2 |Tz| dz),
+//   one more rounding for the difference: eps = 1.1 * 2^-24 (2.8 dmax + 3 zmax + 2 |Tz| dz) with
+//   zmax = max |z| over the volume's corners.  tools/check_f32_filter.c checks the bound on random
+//   poses and voxels against the exact f64 path.
+// ---------------------------------------------------------------------------------------------
+// (host side: tsdf_filter.h, f32_filter_consts)
 
 // v_cvt_i32_f64 clamps out-of-range inputs to INT_MIN / INT_MAX (a C cast would be undefined
 // there, so the instruction is named directly)
@@ -555,63 +557,100 @@ __device__ inline double readlane_f64(double x, int l) {
 // per brick, one per z-half (zoff = 0 or 4) -- twice the waves for small culled lists (sharded
 // volumes), where one brick per wave leaves SIMDs idle, and half the per-lane registers.
 
+__device__ inline int cvt_flr_i32(float x) {  // v_cvt_flr_i32_f32: floor, clamped (NaN: 0)
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // Phases 1-3 of one frame for one part (z-steps zoff .. zoff+NZ-1 of a lane's column): project,
-// gather, depth / truncation test.  ok[k]: step k updates its voxel; fills the packed colour
-// texels and depth - z of every step (dist_of gives the clamped distance; the integrate computes
-// it only where a voxel needs it).  The per-step conditions stay booleans (lane
-// masks in SGPR pairs): their combinations and wave ballots are scalar instructions, not VALU.
+// gather, depth / truncation test, through the certified f32 filter (above).  Per step the outcome
+// is a code, st[k] = -1 (no update), 1 (an update in free space: depth - z >= trunc, dist = 1
+// exactly) or 0 (an update in the band: diff[k] holds the exact f64 depth - z).  Fills the packed
+// colour texels.  dz: the part's z-steps less its first, f32 (exact: differences of f32 world
+// coordinates a few voxels apart).
+// The outcomes travel as values -- the pixel index -1 for "not in front of the camera", a marker in
+// iv for an uncertain pixel, the code st -- not as bool arrays: step masks that live across the
+// uncertain-step and band branches were turned into VGPR booleans by the compiler (a cndmask and a
+// compare per use; +20 % VALU in a first version).  Each mask is recomputed where it is used.
+constexpr int kSlowMark = (int)0x80000001;  // iv of a step whose pixel the f32 filter left uncertain
+
+#ifdef TSDF_DIAG
+// Diagnostic builds only (tools/gpu/diag_pairs.py): how often the integrate's paths run, summed over
+// launches -- 0 part-frames projected, 1 ... with an update, 2 uncertain-pixel steps redone in f64,
+// 3 band steps made exact, 4 part-frames with an uncertain step, 5 free-space skips of the update's
+// quotients, 6 update steps that needed dist, 7 part-frames on the exact (non-canonical) path
+__device__ unsigned long long g_ddiag[8];
+#define TSDF_DDIAG(i) (lane_id() == 0 ? (void)atomicAdd(&g_ddiag[i], 1ull) : (void)0)
+#else
+#define TSDF_DDIAG(i) ((void)0)
+#endif
+
 template <int DK, int CK, int NZ>
 __device__ __forceinline__ void project_part(double trunc, const Frame& fr, double px, double py,
-                                             const double* pzs, double pz_l, int zoff, bool col_in, int nz,
-                                             unsigned (&cpx)[NZ], double (&diff)[NZ], bool (&ok)[NZ]) {
+                                             const double* pzs, double pz_l, const float* dz, int zoff,
+                                             bool col_in, int nz, unsigned (&cpx)[NZ], double (&diff)[NZ],
+                                             float (&st)[NZ]) {
     constexpr int kPz = NZ < 8 ? NZ : 1;
-    // the z term of OpenBLAS's dgemm chain (grid_fusion.py:363-368): exact, it feeds the depth test
+    // the part's first step in f64 -- z by the reference's own dgemm chain (grid_fusion.py:363-368),
+    // x and y with fx, fy and the translation folded in (fold_error) -- then rounded to f32
+    const double pz0 = NZ < 8 ? pzs[0] : readlane_f64(pz_l, zoff);
     const double a2 = fma(fr.T[9], py, fr.T[8] * px);
-    // the pixel's numerators with fx, fy and the translation folded in (fast path only: their
-    // error is bounded on the host, fold_bound, and covered by the boundary margin)
-    const double b0 = fma(fr.Tf[1], py, fma(fr.Tf[0], px, fr.Tf[3]));
-    const double b1 = fma(fr.Tf[5], py, fma(fr.Tf[4], px, fr.Tf[7]));
-    // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the z-steps (no
-    // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
-    // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
-    // the pixel indices leave the f64 domain at once (saturating v_cvt_i32_f64: out-of-range
-    // values clamp to INT_MIN / INT_MAX and fail the unsigned bounds test below), which keeps
-    // two f64 per step out of the registers live across the gathers
-    double zc[NZ];
+    const float Z0 = (float)(fr.T[11] + fma(fr.T[10], pz0, a2));
+    const float X0 = (float)fma(fr.Tf[2], pz0, fma(fr.Tf[1], py, fma(fr.Tf[0], px, fr.Tf[3])));
+    const float Y0 = (float)fma(fr.Tf[6], pz0, fma(fr.Tf[5], py, fma(fr.Tf[4], px, fr.Tf[7])));
+    const float zmin = NZ < 8 ? fr.ff.zmin4 : fr.ff.zmin8;
+    // phase 1: project in f32, two steps per packed instruction; pixel index = floor(s), certain
+    // where s is not within the margin of an integer (|fract(s) - 0.5| < hm32) and z >= zmin
+    float z32[NZ];
     int iu[NZ], iv[NZ];
-    bool in[NZ], slow[NZ], any_slow = false;
+    bool any_slow = false;
 #pragma unroll
-    for (int k = 0; k < NZ; ++k) {
-        const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
-        const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
-        const double rz = __builtin_amdgcn_rcp(z);  // v_rcp_f64, see frame_margin
-        // X*rz + cx with X = x*fx up to the folding error: within |u - cx| * 2^-24.3 + E/z of
-        // the reference's (x*fx)/z + cx, inside the frame_margin boundary margin below where
-        // z > zmin (E/z < margin/4; the high-dword integer test is a conservative z > zmin)
-        const double sx = fma(fma(fr.Tf[2], pz, b0), rz, fr.cx), sy = fma(fma(fr.Tf[6], pz, b1), rz, fr.cy);
-        const double ux = rint(sx), uy = rint(sy);
-        // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
-        // but is invalid either way)
-        const bool fine = (fabs(sx - ux) < fr.half_m) & (fabs(sy - uy) < fr.half_m) &
-                          ((int)(__double_as_longlong(z) >> 32) > fr.zmin_hi);
-        in[k] = col_in & (k < nz) & (z > 0.0);
-        zc[k] = z;
-        iu[k] = cvt_i32_sat(ux);
-        iv[k] = cvt_i32_sat(uy);
-        slow[k] = in[k] & !fine;
-        any_slow |= slow[k];
+    for (int k = 0; k < NZ; k += 2) {
+        const f2 d2 = {dz[k], dz[k + 1]};
+        const f2 zz = pk_fma(d2, f2{fr.ff.Tz32, fr.ff.Tz32}, f2{Z0, Z0});
+        const f2 xx = pk_fma(d2, f2{fr.ff.Tx32, fr.ff.Tx32}, f2{X0, X0});
+        const f2 yy = pk_fma(d2, f2{fr.ff.Ty32, fr.ff.Ty32}, f2{Y0, Y0});
+        const f2 rz = {__builtin_amdgcn_rcpf(zz.x), __builtin_amdgcn_rcpf(zz.y)};
+        const f2 sx = pk_fma(xx, rz, f2{fr.ff.cxh, fr.ff.cxh});
+        const f2 sy = pk_fma(yy, rz, f2{fr.ff.cyh, fr.ff.cyh});
+        const f2 fu = f2{__builtin_amdgcn_fractf(sx.x), __builtin_amdgcn_fractf(sx.y)} - 0.5f;
+        const f2 fv = f2{__builtin_amdgcn_fractf(sy.x), __builtin_amdgcn_fractf(sy.y)} - 0.5f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool inside = col_in & (k + j < nz);
+            const bool zok = zz[j] >= zmin;  // z > 0 certainly
+            const bool fine = zok & (fabsf(fu[j]) < fr.ff.hm32) & (fabsf(fv[j]) < fr.ff.hm32);
+            const bool slow = inside & !fine & !(zz[j] < fr.ff.zrej32);  // (z32 < zrej32: z <= 0 certainly)
+            any_slow |= slow;
+            z32[k + j] = zz[j];
+            const int fu_i = cvt_flr_i32(sx[j]), fv_i = cvt_flr_i32(sy[j]);  // (unconditional: an asm
+            iu[k + j] = inside & zok ? fu_i : -1;                              //  is never if-converted)
+            iv[k + j] = slow ? kSlowMark : fv_i;
+        }
     }
+    // the reference's own f64 arithmetic for the uncertain steps: one wave-uniform branch per step
+    // with an uncertain lane (computed on every lane, kept on the uncertain ones by selects)
+    TSDF_DDIAG(0);
     if (__ballot(any_slow)) {
-        const double a0 = fma(fr.T[1], py, fr.T[0] * px);  // the reference's x / y chains
+        TSDF_DDIAG(4);
+        const double a0 = fma(fr.T[1], py, fr.T[0] * px);
         const double a1 = fma(fr.T[5], py, fr.T[4] * px);
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            if (!slow[k]) continue;
+            if (!__ballot(iv[k] == kSlowMark)) continue;
+            TSDF_DDIAG(2);
             const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
+            const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-            iu[k] = cvt_i32_sat(rint((x * fr.fx) / zc[k] + fr.cx));  // the reference's own operation order
-            iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
+            // (saturating: out-of-range values clamp to INT_MIN / INT_MAX and fail the bounds test;
+            // a NaN only where z is NaN or 0, which fails z > 0)
+            const int eu = cvt_i32_sat(rint((x * fr.fx) / z + fr.cx));
+            const int ev = cvt_i32_sat(rint((y * fr.fy) / z + fr.cy));
+            const bool sl = iv[k] == kSlowMark;
+            iu[k] = sl ? (z > 0.0 ? eu : -1) : iu[k];
+            iv[k] = sl ? ev : iv[k];
         }
     }
     bool cand[NZ];
@@ -619,10 +658,7 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     const int W = fr.W, H = fr.H;
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        // unsigned bounds on the saturated indices (they come from integral, non-NaN values
-        // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
-        // np.linalg.inv: all NaN -- fails z > 0)
-        cand[k] = in[k] & ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
+        cand[k] = ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
         pix[k] = cand[k] ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
     }
     // phase 2: gather depth and colour for every step at once, before the depth test, so
@@ -631,21 +667,41 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     // under the VGPR budget it otherwise does, serialising the latencies.
     const FrameBufs fb = frame_bufs<DK, CK>(fr);
     unsigned draw[NZ];
+    [[maybe_unused]] double dep64[DK == 1 ? NZ : 1];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        draw[k] = depth_raw<DK>(fb, pix[k]);
+        if (DK == 0) draw[k] = depth_raw<DK>(fb, pix[k]);
+        else dep64[k] = buf_ld_f64(fb.depth, (int)pix[k], 0, 0, 0);
         cpx[k] = buf_ld_u32(fb.color, (int)pix[k], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    double dep[NZ];
+    // phase 3: depth / truncation test (grid_fusion.py:278-286) in f32 where certain: diff32 <
+    // t_rej -> no update; >= t_free -> an update with dist = 1; in between (the band) -> exact
 #pragma unroll
-    for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fb, pix[k], draw[k]);
-    // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
+    for (int k = 0; k < NZ; k += 2) {
+        f2 d2;
+        if (DK == 0) d2 = f2{(float)draw[k], (float)draw[k + 1]} * 0.001f;
+        else d2 = f2{(float)dep64[k], (float)dep64[k + 1]};
+        const f2 df = d2 - f2{z32[k], z32[k + 1]};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = k + j;
+            const bool dpos = DK == 0 ? draw[i] != 0u : dep64[i] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
+            // (f64 depth: no f32 bound on its value, so every valid step takes the exact test)
+            const bool mok = cand[i] & dpos & (DK == 1 || df[j] >= fr.ff.t_rej);
+            st[i] = !mok ? -1.0f : (DK == 0 && df[j] >= fr.ff.t_free) ? 1.0f : 0.0f;
+        }
+    }
+    // the band: exact f64 z, depth and difference (grid_fusion.py:278-286), per step with a lane in it
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        diff[k] = dep[k] - zc[k];
-        const bool dpos = DK == 0 ? draw[k] != 0u : dep[k] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
-        ok[k] = cand[k] & dpos & (diff[k] >= -trunc);
+        if (!__ballot(st[k] == 0.0f)) continue;
+        TSDF_DDIAG(3);
+        const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
+        const double z = fr.T[11] + fma(fr.T[10], pz, a2);
+        const double d = DK == 0 ? depth_m<DK>(fb, pix[k], draw[k]) : dep64[k];
+        diff[k] = d - z;
+        st[k] = st[k] != 0.0f ? st[k] : diff[k] < -trunc ? -1.0f : diff[k] < trunc ? 0.0f : 1.0f;
     }
 }
 
@@ -654,58 +710,16 @@ __device__ inline double dist_of(double trunc, double rtrunc, double diff) {
     return fmin(div_rn(diff, trunc, rtrunc), 1.0);
 }
 
-// Hash z-half waves (NZ = 4, the fused hash launch).  The two halves of a brick are waves 2m and
-// 2m+1 of one workgroup (integrate_list with an even wave count per workgroup) and meet in the
-// brick's claim word of the batch (res[b], reset to kResFree by the cull that listed the brick):
-//  * at item start the z-low wave looks the block up (no insert) and publishes the block or
-//    kResMissing; the z-high wave waits for it.  Both then run the frame loop like the dense grid:
-//    no probe state is live inside the loop, so the hash integrate fits the dense grid's registers;
-//  * a missing block's voxels hold the fresh state (tsdf 1, weight 0, colour 0) -- exactly what
-//    the registers start with -- so a half runs its frames without the block, and only a half
-//    that updated a voxel needs one at the end: it claims the word (kResMissing -> kResBusy),
-//    inserts, initialises the other half and the entry words, publishes block | kResNew (or
-//    kResFail when the table or pool is full) and stores; the other half, if it updated a voxel
-//    too, waits for the publication and stores.  A claimer never waits, so every wait ends.  (No
-//    brick of a batch is listed twice and nothing else inserts during a launch, so a block missing
-//    at item start stays missing until one of its own halves inserts it.)
-// Both waves share a workgroup, so workgroup-scope ordering suffices (agent scope would write
-// back and invalidate the XCD's L2 at every claim).
-#ifdef TSDF_HASH_DIAG
-// Diagnostic builds only (tools/gpu/hash_diag.py): counts of the z-half protocol's events, summed
-// over launches: 0 items, 1 z-low re-lookups, 2 of them found, 3 z-high waits at start, 4 their
-// sleep iterations, 5 end claims (inserts), 6 end waits for the claimer, 7 their sleep iterations
-__device__ unsigned long long g_hash_diag[8];
-#define TSDF_HDIAG(i, n) (lane_id() == 0 ? (void)atomicAdd(&g_hash_diag[i], (unsigned long long)(n)) : (void)0)
-#else
-#define TSDF_HDIAG(i, n) ((void)0)
-#endif
-constexpr int kResFree = -1, kResBusy = -2, kResFail = -3, kResMissing = -4;
-constexpr int kResNew = 1 << 30;  // published block | kResNew: inserted by this launch (blocks < 2^30)
-
-__device__ inline int res_load(const int* rp) {
-    return __hip_atomic_load(rp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ inline void res_publish(int* rp, int val) {  // lane 0, after the wave's stores
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane_id() == 0) __hip_atomic_store(rp, val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ inline int res_wait(const int* rp, int busy) {  // the published value once not `busy`
-    int cur = res_load(rp);
-#ifdef TSDF_HASH_DIAG
-    unsigned spins = 0;
-#endif
-    while (cur == busy) {
-        __builtin_amdgcn_s_sleep(1);
-        cur = res_load(rp);
-#ifdef TSDF_HASH_DIAG
-        ++spins;
-#endif
-    }
-#ifdef TSDF_HASH_DIAG
-    TSDF_HDIAG(busy == kResFree ? 4 : 7, spins);
-#endif
-    return cur;
-}
+// Hash z-half waves (NZ = 4, the fused hash launch; round 5).  The cull that lists a brick one
+// launch ahead also finds or inserts its block (cull_find_or_insert: a new block is initialised to
+// (1, 0, 0) with no entries by the cull's wave) and leaves it in the brick's claim word of the batch
+// (res[b]), or kResFail when the table or pool is full.  So both halves of a brick start at once
+// from their block and run like the dense grid's z-halves -- no lookup, no insert, no waiting on the
+// other half inside the integrate (round 4's claim / wait protocol cost the inserting launch 21 %).
+// A block the batch then leaves without an entry is freed at the end of the call (k_free_unused),
+// so the table holds the reference's keys.  A kResFail brick goes whole to the host's exact re-run
+// (listed by its z-low wave).
+constexpr int kResFree = -1, kResFail = -3;
 
 template <bool HASH, int DK, int CK, bool OW1, int NZ>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
@@ -725,10 +739,6 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const double trunc = v.trunc, rtrunc = v.rtrunc;
     const double* const rcp_hbm = v.rcp;
     const bool canon = v.canon != 0;
-    [[maybe_unused]] int cur_pref = kResFree;
-    if constexpr (kHalfHash && TSDF_RES_PREFETCH)  // (issued now, waited for where it is used; the bound check is below)
-        cur_pref = b < v.nb[0] * v.nb[1] * v.nb[2] ? __hip_atomic_load(res + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                                                   : kResFree;
     const int nb12 = v.nb[1] * v.nb[2];
     if (b >= v.nb[0] * nb12) {  // never for a list k_cull wrote; guards the pool against bad input
         if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
@@ -752,56 +762,33 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     double pzs[kPz];
 #pragma unroll
     for (int k = 0; k < kPz; ++k) pzs[k] = readlane_f64(pz_l, k + zoff);
+    // the f32 filter's steps from the part's first (exact in f32); 8-step parts take them per frame
+    float dz[NZ];
+#pragma unroll
+    for (int k = 0; k < NZ; ++k)  // (wave-uniform: scalar registers)
+        dz[k] = NZ < 8 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)(pzs[k % kPz] - pzs[0])))) : 0.0f;
 
     // the brick's storage: dense brick b, or its hash pool block (wave-uniform; 32-bit for the hash,
     // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
     typename std::conditional<HASH, int, long long>::type blk = -1;
     bool is_new = false;
-    [[maybe_unused]] int* const rp = kHalfHash ? res + b : nullptr;
     if constexpr (kHalfHash) {
-        // the cull's lookup (or kResFree), written by the previous launch: a relaxed read issued
-        // with the item's first instructions and used after its setup (a plain block needs no
-        // ordering); a negative value or a block this launch inserted (kResNew) is read again with
-        // acquire semantics
-        int cur = cur_pref;
-        if (!TSDF_RES_PREFETCH || cur < 0 || (cur & kResNew)) cur = res_load(rp);
-        TSDF_HDIAG(0, 1);
-        if (cur >= 0) {
-        } else if (zoff == 0) {  // not found by the cull: the z-low wave looks again, for both halves
-            long long slot = 0, probe = 0;
-            const int r = table_find_or_insert(tab, pack_key(bx, by, bz), ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits),
-                                               false, is_new, slot, probe);
-            cur = r >= 0 ? r : kResMissing;
-            TSDF_HDIAG(1, 1);
-            TSDF_HDIAG(2, r >= 0 ? 1 : 0);
-            res_publish(rp, cur);
-            if (lane == 0) {
-                atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
-                atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
-                atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
+        // the cull's block (written by the previous launch), or kResFail
+        const int cur = __builtin_amdgcn_readfirstlane(res[b]);
+        if (cur == kResFail) {  // no room: the whole brick waits for the host's exact re-run
+            if (zoff == 0 && lane == 0) {
+                const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
+                if ((long long)o < tab.overflow_cap) tab.overflow[o] = entry;
+                atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
             }
-        } else {
-            TSDF_HDIAG(3, 1);
-            cur = res_wait(rp, kResFree);
+            return;
         }
-        if (cur >= 0) {
-            // found -- a block of an earlier launch, or (kResNew: a z-high wave that starts late) the
-            // block its z-low half already inserted, this half initialised to the fresh state before
-            // the publication this acquire-load saw
-            blk = cur & (kResNew - 1);
-            is_new = (cur & kResNew) != 0;
-            if (blk >= tab.max_blocks) {  // never: a table value is one of the pool's blocks
-                if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
-                return;
-            }
-        }  // else missing (or being claimed / failed): blk stays -1, the frames run from the fresh
-           // state (below) and the end of the item claims the block or waits for the claimer
+        if (cur < 0 || cur >= tab.max_blocks) {  // never: the cull writes a block or kResFail
+            if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
+            return;
+        }
+        blk = cur;
     }
-    // (TSDF_OCC_RMW: the entry words this half owns, loaded now and written back at the end only
-    // if the batch set a new bit -- no atomic: no other wave writes them during the launch)
-    [[maybe_unused]] unsigned long long occ_old = 0;
-    if constexpr (kHalfHash && TSDF_OCC_RMW)
-        if (blk >= 0 && !is_new && lane < NZ) occ_old = coh_load(tab.occ + (size_t)blk * kBrickEdge + zoff + lane);
     float ws[NZ], ts[NZ], cs[NZ];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
@@ -815,7 +802,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     constexpr int kH = NZ / 4;
     bool loaded[kH];
 #pragma unroll
-    for (int h = 0; h < kH; ++h) loaded[h] = kHalfHash && blk < 0;  // a missing hash block: fresh state
+    for (int h = 0; h < kH; ++h) loaded[h] = false;
     // voxels updated by any frame of the batch (entry bits of the hash, ST_UNIQUE): per z-step,
     // the OR of the step masks' ballots -- scalar registers and scalar ORs, no per-lane VGPR bit field
     unsigned long long touched[NZ] = {};
@@ -836,12 +823,21 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #endif
         unsigned cpx[NZ];
         double diff[NZ];
+        float stv[NZ];  // -1: no update, 0: an update in the band (diff exact), 1: in free space
+        if constexpr (NZ == 8) {  // (8-step parts: the steps read out of the lanes per frame)
+            const double p0 = readlane_f64(pz_l, zoff);
+#pragma unroll
+            for (int k = 1; k < NZ; ++k) dz[k] = (float)(readlane_f64(pz_l, k + zoff) - p0);
+        }
+        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, dz, zoff, col_in, nz, cpx, diff, stv);
         bool okv[NZ];
-        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
+#pragma unroll
+        for (int k = 0; k < NZ; ++k) okv[k] = stv[k] >= 0.0f;
         bool need[kH];
 #pragma unroll
         for (int h = 0; h < kH; ++h) need[h] = okv[4 * h] | okv[4 * h + 1] | okv[4 * h + 2] | okv[4 * h + 3];
         if (__ballot(need[0] | need[kH - 1]) == 0) continue;
+        TSDF_DDIAG(1);
 #ifdef TSDF_DIAG
         ++d_valid;
 #endif
@@ -926,6 +922,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
         float wnv[NZ], tqv[NZ], cnv[NZ];  // the step's new weight, tsdf and colour (if it updates)
+        if (!fast_c) TSDF_DDIAG(7);
         if (fast_c) {
             // Steps in pairs (k, k+1) on the packed f32 ALU (v_pk_*: two lanes' worth per
             // instruction): w + 1, w * t, the table offset 8 * (w + 1), and the colour channels'
@@ -937,10 +934,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             // Free space (wave-uniform): every updating voxel is at least trunc in front of the
             // surface (dist = min(1, diff / trunc) = 1 exactly) and still holds tsdf 1, so its new
             // tsdf is (w * 1 + 1) / (w + 1) = 1 exactly: the distance and tsdf quotients are skipped
+            // (an updating step that is not near has depth - z >= trunc: dist = 1, project_part)
             bool busy = false;
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) busy |= okv[k] & ((diff[k] < trunc) | (ts[k] != 1.0f));
+            for (int k = 0; k < NZ; ++k) busy |= (stv[k] == 0.0f) | ((stv[k] > 0.0f) & (ts[k] != 1.0f));
             const bool free_space = __ballot(busy) == 0;
+            if (free_space) TSDF_DDIAG(5);
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
                 const f2 w2 = {ws[k], ws[k + 1]};
@@ -966,7 +965,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const double num = (double)wt2[j] + dist_of(trunc, rtrunc, diff[k + j]);
+                        double dist = 1.0;
+                        if (__ballot(stv[k + j] == 0.0f)) {
+                            TSDF_DDIAG(6);
+                            dist = stv[k + j] == 0.0f ? dist_of(trunc, rtrunc, diff[k + j]) : 1.0;
+                        }
+                        const double num = (double)wt2[j] + dist;
                         tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
                         r2[j] = (float)y[j];
                     }
@@ -997,7 +1001,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             for (int k = 0; k < NZ; ++k) {
                 const float w_old = ws[k];
                 const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
-                const double dist = dist_of(trunc, rtrunc, diff[k]);
+                const double dist = stv[k] == 0.0f ? dist_of(trunc, rtrunc, diff[k]) : 1.0;
                 const double num = (double)(w_old * ts[k]) + (OW1 ? dist : fr.ow * dist);
                 if (fast_t) tqv[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
                 else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, rcp_hbm[(int)wn]);
@@ -1027,9 +1031,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            ws[k] = okv[k] ? wnv[k] : ws[k];
-            ts[k] = okv[k] ? tqv[k] : ts[k];
-            cs[k] = okv[k] ? cnv[k] : cs[k];
+            const bool up = stv[k] >= 0.0f;  // (recomputed here: okv does not live across the update)
+            ws[k] = up ? wnv[k] : ws[k];
+            ts[k] = up ? tqv[k] : ts[k];
+            cs[k] = up ? cnv[k] : cs[k];
         }
     }
 #ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
@@ -1042,58 +1047,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         unsigned long long any = 0;
 #pragma unroll
         for (int k = 0; k < NZ; ++k) any |= touched[k];
-        if (any == 0) return;  // this half updated nothing (its block, if any, was looked up in advance)
-        if (blk < 0) {  // missing block, and this half updated a voxel: claim it or wait for the claimer
-            int cur = res_load(rp), old = kResMissing;
-            if (cur == kResMissing) {
-                if (lane == 0)
-                    __hip_atomic_compare_exchange_strong(rp, &old, kResBusy, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-                old = __shfl(old, 0);
-                cur = old;
-            }
-            if (old == kResMissing && cur == kResMissing) {  // this wave claimed the word
-                TSDF_HDIAG(5, 1);
-                long long slot = 0, probe = 0;
-                const int r = table_find_or_insert(tab, pack_key(bx, by, bz),
-                                                   ref_hash<kHalfHash>(bx, by, bz, tab.capacity, tab.int_bits), true,
-                                                   is_new, slot, probe);
-                if (r < 0 || !is_new) {
-                    // r < 0: no space -- the brick waits for the host's exact re-run (nothing written);
-                    // !is_new never happens (the block was missing and only its halves insert it)
-                    if (lane == 0) {
-                        if (r < 0) {
-                            const unsigned long long o = atomicAdd((unsigned long long*)&tab.st->n_overflow, 1ull);
-                            if ((long long)o < tab.overflow_cap) tab.overflow[o] = entry;
-                            atomicAdd(&s_stat[ST_OVERFLOW], 1ull);
-                        } else {
-                            atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
-                        }
-                    }
-                    res_publish(rp, kResFail);
-                    return;
-                }
-                // the other half and every entry word start fresh too
-                const size_t pb = (size_t)r * kBrickVox + (size_t)lane * kBrickEdge + (4 - zoff);
-                *(float4*)(pool.weight + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                *(float4*)(pool.tsdf + pb) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-                *(float4*)(pool.color + pb) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (lane < kBrickEdge) coh_store(tab.occ + (size_t)r * kBrickEdge + lane, 0ull);
-                res_publish(rp, r | kResNew);
-                if (lane == 0) {
-                    atomicAdd(&s_stat[ST_PROBE], (unsigned long long)probe);
-                    atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)probe);
-                    atomicAdd(&s_stat[ST_ALLOC], 1ull);
-                }
-                blk = r;
-            } else {
-                TSDF_HDIAG(6, 1);
-                cur = res_wait(rp, kResBusy);
-                if (cur == kResFail) return;
-                blk = cur & (kResNew - 1);
-            }
-            is_new = true;
-        }
+        if (any == 0) return;  // this half updated nothing
     } else if (blk < 0) {
         return;  // no frame of the batch updated this brick
     }
@@ -1118,11 +1072,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         if (lane < NZ) {
             unsigned long long* o = tab.occ + (size_t)blk * kBrickEdge + zoff + lane;
             if (is_new) coh_store(o, mine);
-            else if (kHalfHash && TSDF_OCC_RMW) {
-                if (mine & ~occ_old) coh_store(o, occ_old | mine);
-            } else if (mine) {
-                atomicOr(o, mine);
-            }
+            else if (mine) atomicOr(o, mine);
         }
     }
     if (lane == 0) atomicAdd(&s_stat[ST_TOUCHED], 1ull);
@@ -1144,12 +1094,18 @@ constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 
 
 // Wave-level append of the kept bricks (lane: brick e, its frame mask) to the sub-list of their cost
 // class (frames kept): one atomicAdd per class with survivors.
-// The fused hash launch's cull also looks every kept brick's block up (one lane per brick, a
-// linear probe of the power-of-two table: about one slot at the bench's load factors) and leaves
-// the block in the brick's claim word, so that the integrate's waves start at once; a brick not
-// found there (a new one -- or one the integrate of the previous batch, running in the same launch,
-// inserts only now) gets kResFree and is looked up again by its z-low wave (integrate_brick).
-__device__ inline int cull_lookup(const Vol& v, const Table& t, unsigned e, unsigned long long* s_stat) {
+// The fused hash launch's cull also finds or inserts every kept brick's block (one lane per brick, a
+// linear probe of the power-of-two table: about one slot at the bench's load factors; a new block
+// from the pool, its key by CAS into the first tombstone or empty slot of the probe) and leaves it
+// in the brick's claim word for the integrate of the next launch (integrate_brick).  Nothing else
+// inserts during a fused launch (its integrate only reads blocks its cull found a launch earlier),
+// and the bricks of a batch are distinct, so a lost CAS is another brick's key: the probe goes on.
+// The cull's wave then initialises its new blocks -- (1, 0, 0) and no entries, 64 lanes per block --
+// and records them for k_free_unused (a block the batch leaves without an entry is freed at the end
+// of the call).  kResFail: the pool or table is full (the brick goes to the host's exact re-run).
+__device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned e, unsigned long long* s_stat,
+                                          bool& fresh) {
+    fresh = false;
     const int nb12 = v.nb[1] * v.nb[2];
     const int bx = (int)e / nb12, r = (int)e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
     const unsigned long long key = pack_key(bx, by, bz);
@@ -1159,24 +1115,48 @@ __device__ inline int cull_lookup(const Vol& v, const Table& t, unsigned e, unsi
     const long long cap = t.capacity, max_blocks = t.max_blocks;
     const long long mask = cap - 1;
     long long s = ref_hash<true>(bx, by, bz, cap, t.int_bits);
+    long long tomb = -1;
+    int blk = -1;
     for (long long n = 0; n < cap; ++n) {
         const unsigned long long k = coh_load(&keys[s]);
         if (k == key) {
-            const int blk = coh_load(&vals[s]);
+            const int b = coh_load(&vals[s]);
             atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
             atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
             atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
-            return (blk >= 0 && blk < max_blocks) ? blk : kResFree;
+            return (b >= 0 && b < max_blocks) ? b : kResFail;  // (a found key's value is always set)
         }
-        if (k == kEmpty) break;
+        if (k == kTomb) {
+            if (tomb < 0) tomb = s;
+        } else if (k == kEmpty) {  // absent: insert at the first tombstone of the probe, else here
+            const long long target = tomb >= 0 ? tomb : s;
+            const unsigned long long expect = tomb >= 0 ? kTomb : kEmpty;
+            if (blk < 0) blk = pool_alloc(t);
+            if (blk < 0) return kResFail;  // pool exhausted
+            if (atomicCAS(&keys[target], expect, key) == expect) {
+                coh_store(&vals[target], blk);
+                const unsigned long long i = atomicAdd((unsigned long long*)&t.st->n_inserted, 1ull);
+                if ((long long)i < t.ins_cap) t.ins_list[i] = (int)e;
+                atomicAdd(&s_stat[ST_ALLOC], 1ull);
+                atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
+                atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
+                atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
+                fresh = true;
+                return blk;
+            }
+            s = target;  // another brick's key took the slot: probe on from it
+            tomb = -1;
+            continue;
+        }
         s = (s + 1) & mask;
     }
-    return kResFree;
+    return kResFail;  // table full (the growth policy keeps it below 31/32)
 }
 
 template <bool HASH>
 __device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* count, unsigned long long* s_stat,
-                                   int* res, unsigned e, unsigned fmask, const Table* tab = nullptr) {
+                                   int* res, unsigned e, unsigned fmask, const Table* tab = nullptr,
+                                   const Pool* pool = nullptr) {
     const int lane = lane_id();
     const int cls = __popc(fmask);
     const unsigned long long any = __ballot(cls != 0);
@@ -1193,10 +1173,26 @@ __device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* 
     if (lane == 0) atomicAdd(&s_stat[ST_VISITED], (unsigned long long)__popcll(any));
     base = __shfl(base, cls);
     const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
+    bool fresh = false;
+    int blk = kResFree;
     if (cls && base + rank < nbk) {
         list[(size_t)(cls - 1) * nbk + base + rank] = (ListEntry)e | ((ListEntry)fmask << 32);
-        // the brick's claim word for this batch: its block when the cull looked it up
-        if (HASH && res) res[e] = tab ? cull_lookup(v, *tab, e, s_stat) : kResFree;
+        // the brick's claim word for this batch: its block (found or inserted), or kResFail
+        if (HASH && res) res[e] = blk = tab ? cull_find_or_insert(v, *tab, e, s_stat, fresh) : kResFree;
+    }
+    if (HASH && res && pool) {  // new blocks start at (1, 0, 0) with no entries: 64 lanes per block
+        for (unsigned long long m = __ballot(fresh); m; m &= m - 1) {
+            const int b = __shfl(blk, __ffsll((long long)m) - 1);
+            const size_t o = (size_t)b * kBrickVox + (size_t)lane * kBrickEdge;
+            const float4 one = make_float4(1.0f, 1.0f, 1.0f, 1.0f), zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            *(float4*)(pool->tsdf + o) = one;
+            *(float4*)(pool->tsdf + o + 4) = one;
+            *(float4*)(pool->weight + o) = zero;
+            *(float4*)(pool->weight + o + 4) = zero;
+            *(float4*)(pool->color + o) = zero;
+            *(float4*)(pool->color + o + 4) = zero;
+            if (lane < kBrickEdge) coh_store(tab->occ + (size_t)b * kBrickEdge + lane, 0ull);
+        }
     }
 }
 
@@ -1216,7 +1212,7 @@ template <bool HASH, bool P2 = false>
 __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Table& tab, ListEntry* list,
                                        unsigned int* count, unsigned long long* stats, int wgi,
                                        unsigned* s_mask, unsigned long long* s_stat, int* res = nullptr,
-                                       int G = 1) {
+                                       int G = 1, const Pool* pool = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), n_waves = (int)(blockDim.x >> 6);
     if (tid < 64 * G) s_mask[tid] = 0u;
@@ -1248,7 +1244,7 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
         const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
         append_kept<HASH>(v, list, count, s_stat, res, (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz),
-                          s_mask[wave * 64 + lane], P2 ? &tab : nullptr);
+                          s_mask[wave * 64 + lane], P2 ? &tab : nullptr, pool);
     }
     __syncthreads();
     flush_stats(s_stat, stats);
@@ -1261,7 +1257,7 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
 template <bool HASH>
 __device__ inline void cull_owned(const Vol& v, const Batch& bt, const Table& tab, ListEntry* list,
                                   unsigned int* count, unsigned long long* stats, int wgi, unsigned* s_mask,
-                                  unsigned long long* s_stat, int* res) {
+                                  unsigned long long* s_stat, int* res, const Pool* pool = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), n_waves = (int)(blockDim.x >> 6);
     if (tid < 64) s_mask[tid] = 0u;
@@ -1277,7 +1273,7 @@ __device__ inline void cull_owned(const Vol& v, const Batch& bt, const Table& ta
         if (have && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
     }
     __syncthreads();
-    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u, &tab);
+    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u, &tab, pool);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
@@ -1673,6 +1669,7 @@ struct Stage {
     long long seq;           // hash: launch number for the pool report (Table::rb)
     int* res_i;              // hash: per-brick claim words of batch k (integrate) and k+1 (cull)
     int* res_c;
+    unsigned* done;          // hash: arrival counter of the launch's integrate and cull workgroups
 };
 
 #ifdef TSDF_WG_TIMES
@@ -1759,7 +1756,8 @@ __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolRepo
         __hip_atomic_store(&r->pool_top, top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&r->free_count, nf - cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&r->n_overflow, coh_load(&st->n_overflow), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        long long listed = 0;  // the batch's cost-class sub-list lengths (the integrate's list)
+        __hip_atomic_store(&r->tombs, coh_load(&st->tombs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        long long listed = 0;  // the cost-class sub-list lengths of the list given (the allocating one)
         if (count)
             for (int c = 1; c <= kMaxBatch; ++c) listed += coh_load(&((unsigned*)count)[c]);
         __hip_atomic_store(&r->listed, listed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1768,10 +1766,10 @@ __device__ inline void commit_pool(PoolState* st, long long max_blocks, PoolRepo
 }
 
 // The voxel hash's three-stage launch (u16 + RGB8, obs_weight 1 as HashTable.integrate): as
-// k_fused, with the hash integrate (one wave per brick, in-kernel find-or-insert) and the pool
-// commit done by the integrate workgroup that finishes last (an arrival counter in the batch's
-// list counters; every workgroup's allocations are complete before it arrives).
-// (z-half waves, two per brick)
+// k_fused, with the hash integrate (z-half waves on the blocks the previous launch's cull found or
+// inserted) and a cull that finds or inserts the blocks of the next batch; the pool commit of the
+// cull's allocations is done by the integrate or cull workgroup that finishes last (an arrival
+// counter; every workgroup's allocations are complete before it arrives).
 #ifndef TSDF_FUSED_HASH_WAVES
 #define TSDF_FUSED_HASH_WAVES 6
 #endif
@@ -1816,21 +1814,24 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
                                             sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i);
         __syncthreads();
         flush_stats(s_stat, stats);
+    } else if (b < sg.gi + sg.gc) {
+        if (tab.owned)
+            cull_owned<true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf, s_stat, sg.res_c,
+                             &pool);
+        else
+            cull_superbrick<true, true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
+                                        s_stat, sg.res_c, sg.cg, &pool);
+    }
+    if (b < sg.gi + sg.gc) {  // the last integrate / cull workgroup commits the launch's allocations
         if (tid == 0) {
             __threadfence();  // this workgroup's allocations and stores before its arrival
-            s_last = atomicAdd(sg.count_i + kDoneWord, 1u) == (unsigned)sg.gi - 1;
+            s_last = atomicAdd(sg.done, 1u) == (unsigned)(sg.gi + sg.gc) - 1;
         }
         __syncthreads();
         if (s_last && tid == 0) {
             __threadfence();
-            commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq, sg.count_i);
+            commit_pool(tab.st, tab.max_blocks, tab.rb, sg.seq, sg.gc ? sg.count_c : nullptr);
         }
-    } else if (b < sg.gi + sg.gc) {
-        if (tab.owned)
-            cull_owned<true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf, s_stat, sg.res_c);
-        else
-            cull_superbrick<true, true>(v, bc, tab, sg.list_c, sg.count_c, stats, b - sg.gi, (unsigned*)s_buf,
-                                        s_stat, sg.res_c, sg.cg);
     } else {
         const int t = b - sg.gi - sg.gc, per = sg.ptx * sg.pty;
         const int f = t / per, r = t - f * per;

@@ -140,6 +140,7 @@ struct tsdf_hash {
     ListEntry* d_list = nullptr;  // re-run list
     int list_cap = 0;
     int* d_res = nullptr;  // fused launches: per-brick claim words, one array per buffer set
+    int* d_ins = nullptr;  // fused launches: bricks their culls inserted since the last k_free_unused
     // A deferred batch launched by the drop-in's per-frame calls (TSDF_DEFER) whose overflow check
     // waits for the next call on the handle (hash_settle): its frames and prepped buffers stay
     // untouched until then, so a skipped brick is still re-run exactly, before any later frame.
@@ -172,7 +173,8 @@ struct tsdf_hash {
     long long recent_growth() const {  // the largest of the recent growths (at least 256 blocks)
         return std::max<long long>({deltas[0], deltas[1], deltas[2], deltas[3], 256});
     }
-    long long tomb_est = 0;       // PoolState::tombs at the last read (only remove() adds tombstones)
+    long long tomb_est = 0;       // PoolState::tombs at the last read or pool report (remove() and
+                                  // k_free_unused add tombstones)
     bool async_pending = false;   // asynchronous launches since the last overflow check
     // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
     // 156-161); TSDF_HASH_MAX_LOAD overrides it for the load-factor sweep (tools/hash_sweep.py)
@@ -184,6 +186,7 @@ struct tsdf_hash {
     // replaced by plain allocations: unmapped, but reserved until destroy (VArray::release)
     std::vector<std::pair<char*, size_t>> retired_va;
     int vmm_fail_at = -1;  // test hook (TSDF_HASH_VMM_FAIL=k): the next growth of array k fails
+    bool async_grow = true;  // test hook (TSDF_HASH_ASYNC_GROW=0): asynchronous calls never grow ahead
     static constexpr size_t kPer[5] = {sizeof(float) * kBrickVox, sizeof(float) * kBrickVox, sizeof(float) * kBrickVox,
                                        sizeof(unsigned long long) * 8, sizeof(int)};
     long long mapped_blocks() const {  // blocks every pool array has memory for
@@ -395,6 +398,33 @@ __global__ void k_free_empty(Table t, const unsigned long long* keys, long long 
     atomicAdd((unsigned long long*)&t.st->tombs, 1ull);
     const unsigned long long f = atomicAdd((unsigned long long*)&t.st->free_count, 1ull);
     coh_store(&t.free_list[f], (int)blk);
+}
+
+// The end of a fused call: the blocks its culls inserted (Table::ins_list) that no frame gave an
+// entry are unlinked and returned to the free list, so the table holds exactly the reference's
+// keys.  A freed slot whose successor is empty becomes empty again (no probe passes through it to a
+// later key); otherwise a tombstone.  Nothing else runs on the table meanwhile (stream order: after
+// the call's last launch, which has no cull).
+__global__ void k_free_unused(Vol v, Table t) {
+    const long long n = min(coh_load(&t.st->n_inserted), t.ins_cap);
+    const int nb12 = v.nb[1] * v.nb[2];
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const int e = t.ins_list[i];
+        const int bx = e / nb12, r = e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
+        const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
+        if (s < 0) continue;
+        const int blk = coh_load(&t.vals[s]);
+        bool used = false;
+        for (int k = 0; k < 8; ++k) used |= coh_load(&t.occ[(size_t)blk * 8 + k]) != 0ull;
+        if (used) continue;
+        const long long nx = s + 1 == t.capacity ? 0 : s + 1;
+        const bool last = coh_load(&t.keys[nx]) == kEmpty;
+        coh_store(&t.vals[s], -1);  // (the empty-slot invariant, k_fill_keys)
+        coh_store(&t.keys[s], last ? kEmpty : kTomb);
+        if (!last) atomicAdd((unsigned long long*)&t.st->tombs, 1ull);
+        const unsigned long long f = atomicAdd((unsigned long long*)&t.st->free_count, 1ull);
+        coh_store(&t.free_list[f], blk);
+    }
 }
 
 __global__ void k_rehash(Table src, Table dst) {
@@ -786,6 +816,7 @@ int wait_report(tsdf_hash* h, long long s, PoolReport* out) {
     out->free_count = r->free_count;
     out->n_overflow = r->n_overflow;
     out->listed = r->listed;
+    out->tombs = r->tombs;
     out->seq = s + 1;
     return TSDF_OK;
 }
@@ -801,8 +832,10 @@ int async_room(tsdf_hash* h, long long s) {
     PoolReport r;
     TSDF_TRY(wait_report(h, s - 2, &r));
     if (r.n_overflow > 0) return take_overflow(h);
+    if (!h->async_grow) return TSDF_OK;
     const long long used = r.pool_top - r.free_count;
     h->note_live(used);
+    h->tomb_est = std::max(h->tomb_est, r.tombs);
     // (the copy path keeps the pool's 1/12 as a floor of the estimate too, and doubles)
     const long long step = h->vmm ? h->recent_growth() : std::max<long long>(h->recent_growth(), h->t.max_blocks / 12);
     const long long need = used + std::max<long long>(3 * step, 2 * r.listed + step);
@@ -870,10 +903,15 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
 }
 
 // Three-stage launches (k_fused_hash; the dense path's scheme, tsdf_dense.hip): launch L
-// integrates batch L, culls L+1 and preps L+2.  Synchronous calls check batch L's overflow
-// before launch L+1 is issued; its re-run reads batch L's frames, which no launch has replaced.
-// The cull of batch L+1 already ran, which a resize cannot invalidate: it reads the table only
-// for shard ownership, fixed at create (Table::shard_cap).
+// integrates batch L, culls L+1 -- finding or inserting its blocks into the claim words res_c --
+// and preps L+2.  Synchronous calls check batch L's overflow before launch L+1 is issued; its
+// re-run reads batch L's frames, which no launch has replaced.
+// Invariant: block ids stay fixed between the cull that writes a claim word and the integrate that
+// reads it.  What the host may run in between keeps them: grow_table rehashes keys, never values;
+// grow_pool maps or copies blocks in place; an overflow re-run only updates or inserts blocks, and
+// the integrate loads every block it is given (a block the cull inserted may have been updated by
+// that re-run).  A future step that renumbers blocks between launches must rerun the cull.  Blocks
+// are freed only after a call's last launch (k_free_unused), when no claim word is pending.
 // Internal flag of hash_run: a synchronous call of at most one batch whose overflow check
 // (hash_after_batch + ensure_room) is left to the next call on the handle (hash_settle).
 constexpr int kCheckLater = 1 << 30;
@@ -893,10 +931,16 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     const int rot = h->set_rot;
     const auto set_of = [rot](int j) { return (j + rot) % kSets; };
     const int nb = (n_frames + nbat - 1) / nbat;
+    // a pending deferred batch uses one buffer set, which the loop's prep of batch 2 would reuse
+    // (its exact re-run reads it): settle it before a call of several batches (round-4 advisor)
+    if (h->pend.on && nb > 1) TSDF_TRY(hash_settle(h));
     if (!h->d_res) {  // each word is written by the cull that lists its brick before an integrate reads it
-        if (h->t.max_blocks >= kResNew || B.n_bricks >= (1ll << 31) / kSets)
-            return set_error(TSDF_E_ARG, "volume too large for the claim words");
+        if (B.n_bricks >= (1ll << 31) / kSets) return set_error(TSDF_E_ARG, "volume too large for the claim words");
         TSDF_HIP(hipMalloc(&h->d_res, sizeof(int) * kSets * (size_t)B.n_bricks));
+        // the bricks the culls insert between two k_free_unused: distinct, so at most every brick
+        TSDF_HIP(hipMalloc(&h->d_ins, sizeof(int) * (size_t)B.n_bricks));
+        h->t.ins_list = h->d_ins;
+        h->t.ins_cap = B.n_bricks;
     }
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
     // (a shard that owns no brick -- more shards than bricks -- still runs one cull workgroup, which
@@ -936,14 +980,19 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
             sg.res_c = h->d_res + (size_t)set_of(L + 1) * B.n_bricks;
         }
         if (has_p) sg.count_p = B.count_set[set_of(jp)];
+        // the arrival counter of the commit (a word the prep of that set reset)
+        sg.done = has_c ? sg.count_c + kDoneWordC : has_i ? sg.count_i + kDoneWord : nullptr;
         const long long grid = (long long)sg.gi + sg.gc + (has_p ? (long long)sg.ptx * sg.pty * bp.n : 0);
         if (grid >= (1ll << 31)) return set_error(TSDF_E_ARG, "fused grid too large");
-        if (has_i) {
-            // the previous deferred batch's overflow check (its report; an exact re-run if it
-            // skipped bricks) comes before this batch's integrate -- after this call's own ingest,
-            // prep and cull were issued, so they overlap the previous batch on the GPU
-            if (h->pend.on) TSDF_TRY(hash_settle(h));
-            if (!sync) TSDF_TRY(async_room(h, h->seq));
+        // the previous deferred batch's overflow check (its report; an exact re-run if it skipped
+        // bricks) comes before this batch's integrate -- after this call's own ingest, prep and cull
+        // were issued, so they overlap the previous batch on the GPU
+        if (has_i && h->pend.on) TSDF_TRY(hash_settle(h));
+        if (has_i || has_c) {
+            // every launch with a cull allocates (its cull inserts the next batch's new blocks) and
+            // every integrate may skip bricks: each such launch reports its pool state
+            if (!sync && has_c) TSDF_TRY(async_room(h, h->seq));
+            if (sync && !has_i) TSDF_TRY(ensure_room(h, true));  // (the call's first cull: last known state)
             sg.seq = h->seq++;
         } else {
             sg.seq = -1;
@@ -974,6 +1023,11 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
             TSDF_TRY(B.end_batch(flags, L % kSlots));
         }
     }
+    // the blocks the call's culls inserted that no frame gave an entry (after the last launch, which
+    // has no cull: no claim word is pending)
+    hipLaunchKernelGGL(k_free_unused, dim3(256), dim3(256), 0, B.stream, B.vol, h->t);
+    TSDF_HIP(hipGetLastError());
+    TSDF_HIP(hipMemsetAsync(&h->t.st->n_inserted, 0, sizeof(long long), B.stream));
     return TSDF_OK;
 }
 
@@ -1065,7 +1119,8 @@ int hash_settle(tsdf_hash* h) {
         h->host_st.free_count = r.free_count;
         h->host_st.n_overflow = 0;
         h->host_st.cursor = 0;
-        h->host_st.tombs = h->tomb_est;  // (only remove() adds tombstones: a synchronous call)
+        h->tomb_est = std::max(h->tomb_est, r.tombs);
+        h->host_st.tombs = h->tomb_est;
         return ensure_room(h, true);
     }
     TSDF_TRY(hash_after_batch(h, h->pend.bt, h->pend.dk, h->pend.ck));
@@ -1237,6 +1292,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
     }
     if (const char* e = getenv("TSDF_PIPELINE")) h->fused = atoi(e) != 0;  // 0: in-line kernels
     if (const char* e = getenv("TSDF_HASH_VMM_FAIL")) h->vmm_fail_at = atoi(e);  // (after the initial mapping)
+    if (const char* e = getenv("TSDF_HASH_ASYNC_GROW")) h->async_grow = atoi(e) != 0;
     if (const char* e = getenv("TSDF_HASH_MAX_LOAD")) {
         const double ml = atof(e);
         if (ml > 0.0 && ml < 1.0) h->max_load = ml;
@@ -1256,7 +1312,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
     if (!h) return TSDF_OK;
     (void)hipSetDevice(h->b.device);
     h->b.release();
-    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res, (void*)h->t.owned};
+    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res, h->d_ins, (void*)h->t.owned};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (h->vmm) {
@@ -1660,17 +1716,6 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 }
 
 }  // extern "C"
-
-#ifdef TSDF_HASH_DIAG
-// (diagnostic builds) the z-half protocol's event counts (g_hash_diag), read and cleared
-extern "C" int tsdf_diag_hash_counts(unsigned long long* out) {
-    TSDF_HIP(hipDeviceSynchronize());
-    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hash_diag), sizeof(unsigned long long) * 8));
-    const unsigned long long zero[8] = {};
-    TSDF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_hash_diag), zero, sizeof(zero)));
-    return TSDF_OK;
-}
-#endif
 
 #ifdef TSDF_WG_TIMES
 // (diagnostic builds) the last fused hash launch's per-workgroup start / end / role|items
