@@ -48,9 +48,10 @@ extern "C" {
                                       of the demos (grid_demo1.py:82: depth_im[depth_im == 65.535] = 0) */
 #define TSDF_DEFER 8        /* tsdf_*_integrate (host frames only): copy the frame into a pinned
                                staging batch and return; the batch runs (asynchronously, as one
-                               temporally batched launch) once it holds a launch's frames
-                               (tsdf_dense_frames_per_launch: 16) or at the next
-                               other call on the handle -- the reference's one-integrate()-per-
+                               temporally batched launch) once it holds 8 frames
+                               (TSDF_DEFER_FRAMES overrides; half a 16-frame launch,
+                               the host's copy grain) or at the next other call
+                               on the handle -- the reference's one-integrate()-per-
                                frame loop (grid_demo1.py:76-87) at batched speed, same results.
                                Hash: a full table / pool found after a deferred batch is grown
                                and its skipped bricks re-run at the next call, before anything

@@ -74,7 +74,6 @@ def test_config3_rank_shard_1000_frames_matches_oracle_rows():
     assert w.max() >= 500 and vol.stats()["list_errors"] == 0
 
 
-@pytest.mark.timeout(400)
 @pytest.fixture(scope="module")
 def bench10k():
     """The bench trajectory's first 10,000 frames in HBM (15 GB: u16 depth bits as int16, RGB8),
@@ -97,6 +96,7 @@ def bench10k():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.timeout(400)
 def test_config3_rank_shard_10000_frames_full_sequence(bench10k):
     """config[3]'s whole sequence on one rank (BASELINE: 10k frames; the demo loop is
     grid_demo1.py:76-87): cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 10,000 frames of
@@ -171,6 +171,7 @@ def test_weights_across_the_reciprocal_table_limit_and_odd_colours(batched, w_lo
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
 
 
+@pytest.mark.timeout(400)
 def test_config4_rank_hash_shard_1024_extent_10000_frames(bench10k):
     """config[4]'s whole per-rank sequence (BASELINE: 10k frames, bucket-range sharded, 1024^3 @
     1 cm; the reference loop is hash_demo1.py:114-125): shard 5 of 8 of a table created with 2^17

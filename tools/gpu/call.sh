@@ -2,13 +2,17 @@
 #   bash tools/gpu/call.sh <out dir under gpurun_out/> <step> [<step> ...]
 # Steps run in order, each under its own time limit; the call stops at the first failure.
 #   tests              pytest -m gpu (in-tree library) + smoke
+#   pytest:<args>      pytest -m gpu <args, '+'-separated> (a subset, e.g. pytest:tests/test_long_gpu.py+-k+config4)
 #   ab:<reps>:<a,b,..> driver-window A/B (tools/gpu/ab_window.py), libraries interleaved <reps>
 #                      times; "base" = in-tree, anything else = abtest/lib<name>.so
+#   abs:<reps>:<a,b,..> tools/gpu/ab.sh: the bench and rank 0 of eighth dense / hash shards, per build
+#                      ("base", abtest/lib<name>.so, or VAR=VAL[+VAR2=VAL2] on the in-tree library)
 #   bench[:<args>]     bench.py --gpus 1 --steps 20 --warmup 5 [args, '+'-separated]
 #   sq[:<lib>]         one rocprofv3 --pmc SQ pass over the dense + hash bench legs
 #   prof               the round profile (tools/gpu/run_round_prof.sh)
 #   py:<script>[:args] python tools/gpu/<script> [args, '+'-separated]
 #   pylib:<lib>:<script>[:args]  the same with TSDF_HIP_LIB=abtest/lib<lib>.so
+#   kt:<script>[:args] the same under rocprofv3 --kernel-trace --stats (stats csv copied to <dir>)
 set -o pipefail
 O="gpurun_out/$1"
 shift
@@ -23,6 +27,11 @@ for step in "$@"; do
         -p no:cacheprovider > "$O/gpu_tests.log" 2>&1 || { echo "tests failed" >> "$O/steps.log"; exit 1; }
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || exit 1
       ;;
+    pytest:*)
+      args=${step#pytest:}; args=${args//+/ }
+      timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        $args > "$O/pytest_subset.log" 2>&1 || { echo "pytest subset failed" >> "$O/steps.log"; exit 1; }
+      ;;
     ab:*)
       IFS=: read -r _ reps names <<< "$step"
       IFS=, read -ra libs <<< "$names"
@@ -31,6 +40,11 @@ for step in "$@"; do
           TSDF_HIP_LIB=$(lib "$n") timeout -k 10 300 python tools/gpu/ab_window.py 3 "$n" >> "$O/ab.jsonl" 2>> "$O/ab.err" || exit 1
         done
       done
+      ;;
+    abs:*)
+      IFS=: read -r _ reps names <<< "$step"
+      IFS=, read -ra libs <<< "$names"
+      bash tools/gpu/ab.sh "$O/abs" "$reps" "${libs[@]}" > "$O/abs.out" 2>&1 || exit 1
       ;;
     bench*)
       args=${step#bench}; args=${args#:}; args=${args//+/ }
@@ -58,6 +72,17 @@ for step in "$@"; do
       IFS=: read -r _ l script args <<< "$step"
       TSDF_HIP_LIB=$(lib "$l") timeout -k 10 600 python -u "tools/gpu/$script" ${args//+/ } > "$O/${script%.py}_$l.out" \
         2> "$O/${script%.py}_$l.err" || exit 1
+      ;;
+    kt:*)
+      IFS=: read -r _ script args <<< "$step"
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kt_${script%.py} -o kt -- \
+        python -u "$R/tools/gpu/$script" ${args//+/ } > "$R/$O/kt_${script%.py}.out" 2> "$R/$O/kt_${script%.py}.err" || exit 1
+      f=$(find /tmp/kt_${script%.py} -name "*kernel_stats.csv" | head -1)
+      [ -n "$f" ] && cp "$f" "$R/$O/kt_${script%.py}_kernel_stats.csv"
+      f=$(find /tmp/kt_${script%.py} -name "*kernel_trace.csv" | head -1)
+      [ -n "$f" ] && cp "$f" "$R/$O/kt_${script%.py}_kernel_trace.csv"
+      cd "$R"
       ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,7 +1,8 @@
 """How often the dense integrate's paths run on the bench workload (TSDF_DIAG build:
 abtest/libdiag.so from tools/build_variant.sh diag -DTSDF_DIAG; TSDF_HIP_LIB selects it):
-part-frames projected and with an update, uncertain-pixel steps of the f32 filter redone in f64,
-band steps made exact, free-space skips, update steps that needed dist, exact-path part-frames.
+part-frames projected and with an update, steps whose pixel the bare-reciprocal fast path left
+uncertain (redone with the reference's division) and the part-frames holding one, free-space skips
+of the update's quotients, exact-path (non-canonical) part-frames.
 
     TSDF_HIP_LIB=abtest/libdiag.so PYTHONPATH=union-thesis-slam_amd python tools/gpu/diag_pairs.py [frames]
 """
@@ -17,8 +18,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
                                 "union-thesis-slam_amd"))
 from tsdf_amd import _ffi, grid_fusion, scene  # noqa: E402
 
-NAMES = ["part_frames", "part_frames_with_update", "uncertain_pixel_steps", "band_steps",
-         "part_frames_with_uncertain", "free_space_skips", "dist_steps", "exact_path_part_frames"]
+NAMES = ["part_frames", "part_frames_with_update", "uncertain_pixel_steps", "part_frames_with_uncertain",
+         "free_space_skips", "exact_path_part_frames", "unused6", "unused7"]
 
 
 def main():

@@ -376,9 +376,15 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
             par_memcpy(hst_depth[slot], d, dbytes * n);
             par_memcpy(hst_color[slot], c, cbytes * n);
         }
+        // (deferred frames: the first pre_copied frames' DMA was issued while the batch filled)
+        const size_t c0 = prestaged >= 0 ? (size_t)std::min(pre_copied, n) : 0;
         TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[slot], 0));
-        TSDF_HIP(hipMemcpyAsync(st_depth[slot], hst_depth[slot], dbytes * n, hipMemcpyHostToDevice, cstream));
-        TSDF_HIP(hipMemcpyAsync(st_color[slot], hst_color[slot], cbytes * n, hipMemcpyHostToDevice, cstream));
+        if (c0 < (size_t)n) {
+            TSDF_HIP(hipMemcpyAsync((char*)st_depth[slot] + dbytes * c0, (const char*)hst_depth[slot] + dbytes * c0,
+                                    dbytes * (n - c0), hipMemcpyHostToDevice, cstream));
+            TSDF_HIP(hipMemcpyAsync((char*)st_color[slot] + cbytes * c0, (const char*)hst_color[slot] + cbytes * c0,
+                                    cbytes * (n - c0), hipMemcpyHostToDevice, cstream));
+        }
         TSDF_HIP(hipEventRecord(ev_copied[slot], cstream));
         TSDF_HIP(hipStreamWaitEvent(stream, ev_copied[slot], 0));
         d = (const char*)st_depth[slot];
@@ -405,22 +411,24 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->fy = (double)(float)K[4];
         fr->cx = (double)(float)K[2];
         fr->cy = (double)(float)K[5];
+        const double margin = frame_margin(W, H, fr->cx, fr->cy);
+        fr->half_m = 0.5 - margin;
         for (int j = 0; j < 4; ++j) {
             fr->Tf[j] = T[j] * fr->fx;
             fr->Tf[4 + j] = T[4 + j] * fr->fy;
         }
-        {  // the certified f32 filter's constants (csrc/tsdf_device.h, f32_filter_consts): the
-           // volume's world box (global voxel indices of this shard's extent) and coordinate bounds
-            double lo[3], hi[3], wmax[3];
+        {  // the fast path's depth limit (fold_bound) as the high dword of a positive f64, rounded up
+            double wmax[3];
             for (int a = 0; a < 3; ++a) {
-                const long long g0 = (long long)vol.off[a];
-                const long long g1 = (a == 0 ? (long long)vol.off[0] + col_gx(vol, vol.nb[0] - 1) + kBrickEdge - 1
-                                             : (long long)vol.off[a] + vol.dims[a] - 1);
-                lo[a] = (double)vol.origin[a] + vol.vs * (double)g0;
-                hi[a] = (double)vol.origin[a] + vol.vs * (double)g1;
-                wmax[a] = fmax(fabs(lo[a]), fabs(hi[a])) + vol.vs + 1.0;
+                const long long gmax = (a == 0 ? (long long)vol.off[0] + col_gx(vol, vol.nb[0] - 1) + kBrickEdge
+                                               : (long long)vol.off[a] + vol.dims[a]);
+                wmax[a] = fabs((double)vol.origin[a]) + vol.vs * (double)gmax + 1.0;
             }
-            f32_filter_consts(&fr->ff, T, fr->Tf, fr->fx, fr->fy, fr->cx, fr->cy, W, H, lo, hi, wmax, vol.vs, vol.trunc);
+            const double zmin = fold_bound(T, fr->fx, fr->fy, wmax, margin);
+            long long bits;
+            std::memcpy(&bits, &zmin, sizeof bits);
+            const long long hi = (std::isfinite(zmin) && zmin < 1e300) ? (bits >> 32) + 1 : 0x7FEFFFFFll;
+            fr->zmin_hi = (int)std::min<long long>(hi, 0x7FEFFFFFll);
         }
         fr->ow = ow ? ow[first + i] : ow_default;
         fr->ow32 = (float)fr->ow;
@@ -475,6 +483,7 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
     if (dfr.n == 0) {
         TSDF_TRY(stage_alloc(dbytes, cbytes));
         dfr.slot = defer_next;
+        dfr.copied = 0;
         defer_next = (defer_next + 1) % kSlots;
         TSDF_HIP(hipEventSynchronize(ev_copied[dfr.slot]));  // its previous DMA has finished
         dfr.dk = dk;
@@ -489,6 +498,17 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
     std::memcpy(dfr.T + 16 * i, T, 16 * sizeof(double));
     dfr.ow[i] = ow;
     dfr.n = i + 1;
+    if (dfr.n * 2 == defer_frames && dfr.n >= 2) {
+        // half the batch collected: its DMA starts now (one transfer per field), so that at the
+        // flush only the other half is still to cross PCIe before the batch's launches can run --
+        // the hash flush waits for the previous batch's pool report, i.e. for that batch's whole
+        // DMA + launches, which with one DMA per batch took longer than the host's copies of the
+        // next 8 frames (profiles/r05_dropin/)
+        TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[dfr.slot], 0));
+        TSDF_HIP(hipMemcpyAsync(st_depth[dfr.slot], hst_depth[dfr.slot], dbytes * dfr.n, hipMemcpyHostToDevice, cstream));
+        TSDF_HIP(hipMemcpyAsync(st_color[dfr.slot], hst_color[dfr.slot], cbytes * dfr.n, hipMemcpyHostToDevice, cstream));
+        dfr.copied = dfr.n;
+    }
     return TSDF_OK;
 }
 

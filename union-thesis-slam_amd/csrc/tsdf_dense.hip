@@ -157,12 +157,18 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
         for (int i = 0; i < bi.n; ++i) ow1 = ow1 && bi.f[i].ow == 1.0;
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
-        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0) | (dk == TSDF_DEPTH_U16_MM ? 0 : 4);
+        // (u32 colour registers where the volume is canonical: obs_weight 1 and NZ = 4, tsdf_device.h)
+        const bool cu = TSDF_COLOR_U32 && ow1 && h->nz == 4 && B.vol.canon;
+        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0) | (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (cu ? 8 : 0);
         const FusedArgs args{B.vol, bi, bc, bp, B.pool, B.stats, sg};
         switch (sel) {
 #define TSDF_LAUNCH(S, OW_, NZ_, DK_)                                                                   \
     case S:                                                                                             \
         hipLaunchKernelGGL((k_fused<OW_, NZ_, DK_>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, args); \
+        break;
+#define TSDF_LAUNCH_CU(S, OW_, NZ_, DK_)                                                                \
+    case S:                                                                                             \
+        hipLaunchKernelGGL((k_fused<OW_, NZ_, DK_, true>), dim3((unsigned)grid), dim3(kFusedWG), 0, B.stream, args); \
         break;
             TSDF_LAUNCH(0, false, 8, 0)
             TSDF_LAUNCH(1, true, 8, 0)
@@ -172,7 +178,10 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
             TSDF_LAUNCH(5, true, 8, 1)
             TSDF_LAUNCH(6, false, 4, 1)
             TSDF_LAUNCH(7, true, 4, 1)
+            TSDF_LAUNCH_CU(11, true, 4, 0)
+            TSDF_LAUNCH_CU(15, true, 4, 1)
 #undef TSDF_LAUNCH
+#undef TSDF_LAUNCH_CU
         }
         TSDF_HIP(hipGetLastError());
         if (has_i) {
@@ -213,9 +222,11 @@ int dense_flush(tsdf_dense* h) {
     const Base::Deferred d = B.dfr;
     B.dfr.n = 0;
     B.prestaged = d.slot;
+    B.pre_copied = d.copied;
     const int r = dense_run(h, d.n, B.hst_depth[d.slot], d.dk, B.hst_color[d.slot], d.ck, d.H, d.W, d.K, d.T,
                             d.ow, TSDF_ASYNC);
     B.prestaged = -1;
+    B.pre_copied = 0;
     return r;
 }
 

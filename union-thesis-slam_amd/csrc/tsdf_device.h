@@ -16,8 +16,6 @@
 #include <stdint.h>
 #include <type_traits>
 
-#include "tsdf_filter.h"
-
 namespace tsdf {
 
 constexpr int kBrickEdge = 8;
@@ -63,12 +61,9 @@ struct Frame {
     double T[12];             // rows 0..2 of inv(cam_pose), row-major
     double fx, fy, cx, cy;    // f64(f32(K))  (cam2pix casts intr to float32, grid_fusion.py:190)
     double ow;                // obs_weight as a Python float (f64)
-    double Tf[8];             // the f32 filter's x / y rows: RN(T[0..3] * fx), RN(T[4..7] * fy)
-    // The certified f32 filter (project_part; host: f32_filter_consts): per step,
-    // camera z and the pixel numerators in f32 from the part's first step, Z_k = Z0 + Tz32 * dz_k,
-    // X_k = X0 + Tx32 * dz_k, Y_k = Y0 + Ty32 * dz_k, and s = X_k * rcp(Z_k) + (cx + 0.5).  Every
-    // decision is taken in f32 only where its error bound makes it certain; the rest is redone in f64.
-    F32Filter ff;
+    double half_m;            // 0.5 - the fast pixel path's boundary margin (frame_margin)
+    double Tf[8];             // the fast pixel path's rows: RN(T[0..3] * fx), RN(T[4..7] * fy)
+    int zmin_hi;              // ... and its depth limit: high dword of zmin (fold_bound, host)
     float ow32;               // the same weight as NumPy's weak-scalar f32 (colour blend)
     int H, W;
     const void* depth;        // depth read by cull/integrate: u16 millimetres or f64 metres
@@ -116,10 +111,23 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
+#ifndef TSDF_RCP_SHARE  // project_part: one reciprocal per four z-steps
+#define TSDF_RCP_SHARE 0
+#endif
+#ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU)
+#define TSDF_COLOR_U32 0
+#endif
+#ifndef TSDF_PAIR_SKIP  // fast update: skip step pairs that no lane of the wave updates
+#define TSDF_PAIR_SKIP 0
+#endif
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); words kDoneWord / kDoneWordC = integrate and cull workgroups finished (fused hash
-// launch; the launch counts on its cull's set, or on its integrate's set when it has no cull).
-constexpr int kCountWords = 32, kDoneWord = 24, kDoneWordC = 25;
+// launch; the launch counts on its cull's set, or on its integrate's set when it has no cull);
+// words kQueueWord .. +7 = the fused integrate's per-XCD item queues (TSDF_GLOBAL_TAKE).
+constexpr int kCountWords = 48, kDoneWord = 24, kDoneWordC = 25, kQueueWord = 32;
+#ifndef TSDF_GLOBAL_TAKE  // fused launches: integrate items taken from per-XCD queues (integrate_items)
+#define TSDF_GLOBAL_TAKE 0
+#endif
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 // The whole table in HBM (512 KB, L2-resident) for waves with a weight past the LDS part (long
 // runs: weights pass 4079 after ~4300 frames of a room seen from inside); 65536 keeps every colour
@@ -471,6 +479,13 @@ __device__ inline double depth_m(const FrameBufs& fb, unsigned p, unsigned raw) 
     return buf_ld_f64(fb.depth, (int)p, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Reciprocal of z for the fast pixel path: the bare v_rcp_f64, accurate to 2^-24.4 relative
+// (random z in [1e-3, 1e3] and a 2^28-point mantissa sweep: tools/gpu/rcp_probe.hip), so
+// u = (x*fx)*rz + cx lies within |u - cx| * 2^-24.3 of the reference's (x*fx)/z + cx (< 3e-5 px
+// for 640x480).  Steps whose u is within frame_margin of a rounding boundary (or not finite) are recomputed with the reference's own division (a Newton-refined reciprocal
+// with a 1e-9 px margin ran 2.6 % slower: the two FMAs cost more than the extra slow steps).
+// ---------------------------------------------------------------------------------------------
 // RN(a / b) given y = RN(1 / b): Markstein's correction step.  q0 = RN(a*y) is within 1 ulp
 // of a/b, r = a - b*q0 is exact with an FMA, and RN(q0 + r*y) is then the correctly rounded
 // quotient (Markstein 1990; Muller et al., Handbook of Floating-Point Arithmetic, "Markstein's
@@ -499,34 +514,29 @@ __device__ inline f2 div_rn32x2(f2 a, f2 b, f2 y) {  // div_rn32 on both lanes
     return pk_fma(r, y, q0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The certified f32 filter (round 5).  The reference projects every voxel in f64 (SURVEY §8(a)
-// a4-a6): z, then u = rint((x*fx)/z + cx), v likewise, and tests z > 0, the bounds, depth > 0,
-// depth - z >= -trunc.  Of those f64 values the result needs exactly only the decisions and, for
-// voxels in the truncation band, depth - z itself (dist = min(1, (depth - z) / trunc) is 1 exactly
-// wherever depth - z >= trunc, i.e. in free space).  So every step is first classified in f32 --
-// camera z and the pixel numerators stepped from the part's first step, one v_rcp_f32, packed
-// arithmetic two steps per instruction -- and a decision is taken there only where the f32 error
-// bound below makes it certain; a pixel coordinate within the margin of a rounding boundary (or z
-// below zmin) is redone with the reference's f64 division, and a step in the band (or near either
-// truncation limit) gets its exact f64 z, depth and difference.  Results are bit-identical to the
-// f64 path: the f32 values only ever choose between outcomes that the bound proves equal.
-//
-// Error bound (host, f32_filter_consts), per pixel axis with focal f, centre c, image side N, for a
-// step with z >= zmin whose pixel is within a pixel of the image (q = max(|c|, |N - c|) + 1.5 bounds
-// |X / Z|; farther pixels are out of bounds whichever way they round):
-//   X0 = RN32(X(pz0)) (f64 chain, then one rounding), X_k = RN32(Tx32 * dz_k + X0): |X_k - X| <=
-//   2^-24 (2|X| + 2|Tx| dz) with dz <= (steps - 1) * vs; Z likewise with |Tz|; rcp_f32 <= 1 ulp;
-//   s = RN32(X_k * r + RN32(c + 0.5)) adds 2^-24 (q + 1.5 (|c| + 0.5)).  So
-//     |s - (X / Z + c + 0.5)| <= 1.01 * 2^-24 (7 q + 1.5 (|c| + 0.5) + 2 dz (|Tx| + q |Tz|) / zmin)
-//   plus the f64 folding error of X0 (fold_error / zmin).  The margin is 1.1 x that; zmin keeps the
-//   dz term at half the rest (640x480, 2 cm voxels: margin 2.8e-4 px, zmin 0.08 m for 4-step parts).
-//   depth - z: |d32 - d| <= 1.8 * 2^-24 d (u16 * 0.001f), |Z_k - z| <= 2^-24 (2 |z| + 2 |Tz| dz),
-//   one more rounding for the difference: eps = 1.1 * 2^-24 (2.8 dmax + 3 zmax + 2 |Tz| dz) with
-//   zmax = max |z| over the volume's corners.  tools/check_f32_filter.c checks the bound on random
-//   poses and voxels against the exact f64 path.
-// ---------------------------------------------------------------------------------------------
-// (host side: tsdf_filter.h, f32_filter_consts)
+// The fast path's pixel error is < |u - c| * 2^-24.3 (the bare reciprocal), and wherever the
+// boundary test matters |u - c| <= max(W, H) + max(|cx|, |cy|) -- a step closer than this margin to
+// a rounding boundary takes the exact path.  1e-4 px covers images up to ~1000 px; larger ones
+// scale it.  Host-side: stored per frame as half_m = 0.5 - margin.
+inline double frame_margin(int W, int H, double cx, double cy) {
+    const double span = (double)(W > H ? W : H) + fmax(fabs(cx), fabs(cy));
+    return fmax(1e-4, 1e-7 * span);
+}
+
+// The fast path folds fx, fy and the translation into its rows: X = fma(Tf2, pz, fma(Tf1, py,
+// fma(Tf0, px, Tf3))) with Tf = RN(T * f) -- four roundings, each within 2^-53 of its operands'
+// magnitudes, so |X - f * x| <= E = 8 * 2^-53 * f * (|T0| X + |T1| Y + |T2| Z + |T3|) for world
+// coordinates bounded by (X, Y, Z) (a factor 2 of slack).  Its pixel error E / z stays below a
+// quarter of the margin where z > zmin = 4 E / margin.  Returns zmin (host).
+inline double fold_bound(const double* T, double fx, double fy, const double wmax[3], double margin) {
+    double e = 0.0;
+    for (int r = 0; r < 2; ++r) {
+        const double* t = T + 4 * r;
+        const double s = fabs(t[0]) * wmax[0] + fabs(t[1]) * wmax[1] + fabs(t[2]) * wmax[2] + fabs(t[3]);
+        e = fmax(e, 8.0 * 0x1p-53 * (r == 0 ? fx : fy) * s);
+    }
+    return 4.0 * e / margin;
+}
 
 // v_cvt_i32_f64 clamps out-of-range inputs to INT_MIN / INT_MAX (a C cast would be undefined
 // there, so the instruction is named directly)
@@ -557,100 +567,100 @@ __device__ inline double readlane_f64(double x, int l) {
 // per brick, one per z-half (zoff = 0 or 4) -- twice the waves for small culled lists (sharded
 // volumes), where one brick per wave leaves SIMDs idle, and half the per-lane registers.
 
-__device__ inline int cvt_flr_i32(float x) {  // v_cvt_flr_i32_f32: floor, clamped (NaN: 0)
-    int r;
-    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
-    return r;
-}
-
-// Phases 1-3 of one frame for one part (z-steps zoff .. zoff+NZ-1 of a lane's column): project,
-// gather, depth / truncation test, through the certified f32 filter (above).  Per step the outcome
-// is a code, st[k] = -1 (no update), 1 (an update in free space: depth - z >= trunc, dist = 1
-// exactly) or 0 (an update in the band: diff[k] holds the exact f64 depth - z).  Fills the packed
-// colour texels.  dz: the part's z-steps less its first, f32 (exact: differences of f32 world
-// coordinates a few voxels apart).
-// The outcomes travel as values -- the pixel index -1 for "not in front of the camera", a marker in
-// iv for an uncertain pixel, the code st -- not as bool arrays: step masks that live across the
-// uncertain-step and band branches were turned into VGPR booleans by the compiler (a cndmask and a
-// compare per use; +20 % VALU in a first version).  Each mask is recomputed where it is used.
-constexpr int kSlowMark = (int)0x80000001;  // iv of a step whose pixel the f32 filter left uncertain
-
 #ifdef TSDF_DIAG
 // Diagnostic builds only (tools/gpu/diag_pairs.py): how often the integrate's paths run, summed over
-// launches -- 0 part-frames projected, 1 ... with an update, 2 uncertain-pixel steps redone in f64,
-// 3 band steps made exact, 4 part-frames with an uncertain step, 5 free-space skips of the update's
-// quotients, 6 update steps that needed dist, 7 part-frames on the exact (non-canonical) path
+// launches -- 0 part-frames projected, 1 ... with an update, 2 steps whose pixel was redone with the
+// reference's division, 3 part-frames with such a step, 4 free-space skips of the update's
+// quotients, 5 part-frames on the exact (non-canonical) path
 __device__ unsigned long long g_ddiag[8];
 #define TSDF_DDIAG(i) (lane_id() == 0 ? (void)atomicAdd(&g_ddiag[i], 1ull) : (void)0)
 #else
 #define TSDF_DDIAG(i) ((void)0)
 #endif
 
+// Phases 1-3 of one frame for one part (z-steps zoff .. zoff+NZ-1 of a lane's column): project,
+// gather, depth / truncation test.  ok[k]: step k updates its voxel; fills the packed colour
+// texels and depth - z of every step (dist_of gives the clamped distance; the integrate computes
+// it only where a voxel needs it).  The per-step conditions stay booleans (lane
+// masks in SGPR pairs): their combinations and wave ballots are scalar instructions, not VALU.
 template <int DK, int CK, int NZ>
 __device__ __forceinline__ void project_part(double trunc, const Frame& fr, double px, double py,
-                                             const double* pzs, double pz_l, const float* dz, int zoff,
-                                             bool col_in, int nz, unsigned (&cpx)[NZ], double (&diff)[NZ],
-                                             float (&st)[NZ]) {
+                                             const double* pzs, double pz_l, int zoff, bool col_in, int nz,
+                                             unsigned (&cpx)[NZ], double (&diff)[NZ], bool (&ok)[NZ]) {
     constexpr int kPz = NZ < 8 ? NZ : 1;
-    // the part's first step in f64 -- z by the reference's own dgemm chain (grid_fusion.py:363-368),
-    // x and y with fx, fy and the translation folded in (fold_error) -- then rounded to f32
-    const double pz0 = NZ < 8 ? pzs[0] : readlane_f64(pz_l, zoff);
+    // the z term of OpenBLAS's dgemm chain (grid_fusion.py:363-368): exact, it feeds the depth test
     const double a2 = fma(fr.T[9], py, fr.T[8] * px);
-    const float Z0 = (float)(fr.T[11] + fma(fr.T[10], pz0, a2));
-    const float X0 = (float)fma(fr.Tf[2], pz0, fma(fr.Tf[1], py, fma(fr.Tf[0], px, fr.Tf[3])));
-    const float Y0 = (float)fma(fr.Tf[6], pz0, fma(fr.Tf[5], py, fma(fr.Tf[4], px, fr.Tf[7])));
-    const float zmin = NZ < 8 ? fr.ff.zmin4 : fr.ff.zmin8;
-    // phase 1: project in f32, two steps per packed instruction; pixel index = floor(s), certain
-    // where s is not within the margin of an integer (|fract(s) - 0.5| < hm32) and z >= zmin
-    float z32[NZ];
+    // the pixel's numerators with fx, fy and the translation folded in (fast path only: their
+    // error is bounded on the host, fold_bound, and covered by the boundary margin)
+    const double b0 = fma(fr.Tf[1], py, fma(fr.Tf[0], px, fr.Tf[3]));
+    const double b1 = fma(fr.Tf[5], py, fma(fr.Tf[4], px, fr.Tf[7]));
+    // phase 1: project (grid_fusion.py:262-277).  Straight-line code over the z-steps (no
+    // per-step branches) so the compiler can interleave their f64 chains; the rare steps whose
+    // pixel lies within frame_margin of a rounding boundary are redone exactly afterwards.
+    // the pixel indices leave the f64 domain at once (saturating v_cvt_i32_f64: out-of-range
+    // values clamp to INT_MIN / INT_MAX and fail the unsigned bounds test below), which keeps
+    // two f64 per step out of the registers live across the gathers
+    double zc[NZ];
     int iu[NZ], iv[NZ];
-    bool any_slow = false;
+    bool in[NZ], slow[NZ], any_slow = false;
 #pragma unroll
-    for (int k = 0; k < NZ; k += 2) {
-        const f2 d2 = {dz[k], dz[k + 1]};
-        const f2 zz = pk_fma(d2, f2{fr.ff.Tz32, fr.ff.Tz32}, f2{Z0, Z0});
-        const f2 xx = pk_fma(d2, f2{fr.ff.Tx32, fr.ff.Tx32}, f2{X0, X0});
-        const f2 yy = pk_fma(d2, f2{fr.ff.Ty32, fr.ff.Ty32}, f2{Y0, Y0});
-        const f2 rz = {__builtin_amdgcn_rcpf(zz.x), __builtin_amdgcn_rcpf(zz.y)};
-        const f2 sx = pk_fma(xx, rz, f2{fr.ff.cxh, fr.ff.cxh});
-        const f2 sy = pk_fma(yy, rz, f2{fr.ff.cyh, fr.ff.cyh});
-        const f2 fu = f2{__builtin_amdgcn_fractf(sx.x), __builtin_amdgcn_fractf(sx.y)} - 0.5f;
-        const f2 fv = f2{__builtin_amdgcn_fractf(sy.x), __builtin_amdgcn_fractf(sy.y)} - 0.5f;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const bool inside = col_in & (k + j < nz);
-            const bool zok = zz[j] >= zmin;  // z > 0 certainly
-            const bool fine = zok & (fabsf(fu[j]) < fr.ff.hm32) & (fabsf(fv[j]) < fr.ff.hm32);
-            const bool slow = inside & !fine & !(zz[j] < fr.ff.zrej32);  // (z32 < zrej32: z <= 0 certainly)
-            any_slow |= slow;
-            z32[k + j] = zz[j];
-            const int fu_i = cvt_flr_i32(sx[j]), fv_i = cvt_flr_i32(sy[j]);  // (unconditional: an asm
-            iu[k + j] = inside & zok ? fu_i : -1;                              //  is never if-converted)
-            iv[k + j] = slow ? kSlowMark : fv_i;
-        }
+    for (int k = 0; k < NZ; ++k) {
+        const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
+        zc[k] = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
     }
-    // the reference's own f64 arithmetic for the uncertain steps: one wave-uniform branch per step
-    // with an uncertain lane (computed on every lane, kept on the uncertain ones by selects)
+    double rzs[NZ];
+#if TSDF_RCP_SHARE
+    // one v_rcp_f64 (10.5 issue cycles, four FMAs' worth) per four steps: r = rcp(z0 z1 z2 z3),
+    // 1/(z0 z1) = (z2 z3) r, 1/z0 = z1 / (z0 z1) ...  -- the rcp's 2^-24.4 relative error plus a few
+    // f64 roundings, inside the margin's 2^-24.3; a zero or non-finite z makes its group's
+    // quotients non-finite, which the boundary test sends to the exact path
+#pragma unroll
+    for (int k = 0; k < NZ; k += 4) {
+        const double z01 = zc[k] * zc[k + 1], z23 = zc[k + 2] * zc[k + 3];
+        const double r = __builtin_amdgcn_rcp(z01 * z23);
+        const double r01 = z23 * r, r23 = z01 * r;
+        rzs[k] = zc[k + 1] * r01;
+        rzs[k + 1] = zc[k] * r01;
+        rzs[k + 2] = zc[k + 3] * r23;
+        rzs[k + 3] = zc[k + 2] * r23;
+    }
+#else
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) rzs[k] = __builtin_amdgcn_rcp(zc[k]);  // v_rcp_f64, see frame_margin
+#endif
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
+        const double z = zc[k], rz = rzs[k];
+        // X*rz + cx with X = x*fx up to the folding error: within |u - cx| * 2^-24.3 + E/z of
+        // the reference's (x*fx)/z + cx, inside the frame_margin boundary margin below where
+        // z > zmin (E/z < margin/4; the high-dword integer test is a conservative z > zmin)
+        const double sx = fma(fma(fr.Tf[2], pz, b0), rz, fr.cx), sy = fma(fma(fr.Tf[6], pz, b1), rz, fr.cy);
+        const double ux = rint(sx), uy = rint(sy);
+        // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
+        // but is invalid either way)
+        const bool fine = (fabs(sx - ux) < fr.half_m) & (fabs(sy - uy) < fr.half_m) &
+                          ((int)(__double_as_longlong(z) >> 32) > fr.zmin_hi);
+        in[k] = col_in & (k < nz) & (z > 0.0);
+        iu[k] = cvt_i32_sat(ux);
+        iv[k] = cvt_i32_sat(uy);
+        slow[k] = in[k] & !fine;
+        any_slow |= slow[k];
+    }
     TSDF_DDIAG(0);
     if (__ballot(any_slow)) {
-        TSDF_DDIAG(4);
-        const double a0 = fma(fr.T[1], py, fr.T[0] * px);
+        TSDF_DDIAG(3);
+        const double a0 = fma(fr.T[1], py, fr.T[0] * px);  // the reference's x / y chains
         const double a1 = fma(fr.T[5], py, fr.T[4] * px);
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            if (!__ballot(iv[k] == kSlowMark)) continue;
+            if (!slow[k]) continue;
             TSDF_DDIAG(2);
             const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
-            const double z = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
             const double y = fr.T[7] + fma(fr.T[6], pz, a1);
-            // (saturating: out-of-range values clamp to INT_MIN / INT_MAX and fail the bounds test;
-            // a NaN only where z is NaN or 0, which fails z > 0)
-            const int eu = cvt_i32_sat(rint((x * fr.fx) / z + fr.cx));
-            const int ev = cvt_i32_sat(rint((y * fr.fy) / z + fr.cy));
-            const bool sl = iv[k] == kSlowMark;
-            iu[k] = sl ? (z > 0.0 ? eu : -1) : iu[k];
-            iv[k] = sl ? ev : iv[k];
+            iu[k] = cvt_i32_sat(rint((x * fr.fx) / zc[k] + fr.cx));  // the reference's own operation order
+            iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
         }
     }
     bool cand[NZ];
@@ -658,7 +668,10 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     const int W = fr.W, H = fr.H;
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        cand[k] = ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
+        // unsigned bounds on the saturated indices (they come from integral, non-NaN values
+        // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
+        // np.linalg.inv: all NaN -- fails z > 0)
+        cand[k] = in[k] & ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
         pix[k] = cand[k] ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
     }
     // phase 2: gather depth and colour for every step at once, before the depth test, so
@@ -667,41 +680,21 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     // under the VGPR budget it otherwise does, serialising the latencies.
     const FrameBufs fb = frame_bufs<DK, CK>(fr);
     unsigned draw[NZ];
-    [[maybe_unused]] double dep64[DK == 1 ? NZ : 1];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        if (DK == 0) draw[k] = depth_raw<DK>(fb, pix[k]);
-        else dep64[k] = buf_ld_f64(fb.depth, (int)pix[k], 0, 0, 0);
+        draw[k] = depth_raw<DK>(fb, pix[k]);
         cpx[k] = buf_ld_u32(fb.color, (int)pix[k], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // phase 3: depth / truncation test (grid_fusion.py:278-286) in f32 where certain: diff32 <
-    // t_rej -> no update; >= t_free -> an update with dist = 1; in between (the band) -> exact
+    double dep[NZ];
 #pragma unroll
-    for (int k = 0; k < NZ; k += 2) {
-        f2 d2;
-        if (DK == 0) d2 = f2{(float)draw[k], (float)draw[k + 1]} * 0.001f;
-        else d2 = f2{(float)dep64[k], (float)dep64[k + 1]};
-        const f2 df = d2 - f2{z32[k], z32[k + 1]};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int i = k + j;
-            const bool dpos = DK == 0 ? draw[i] != 0u : dep64[i] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
-            // (f64 depth: no f32 bound on its value, so every valid step takes the exact test)
-            const bool mok = cand[i] & dpos & (DK == 1 || df[j] >= fr.ff.t_rej);
-            st[i] = !mok ? -1.0f : (DK == 0 && df[j] >= fr.ff.t_free) ? 1.0f : 0.0f;
-        }
-    }
-    // the band: exact f64 z, depth and difference (grid_fusion.py:278-286), per step with a lane in it
+    for (int k = 0; k < NZ; ++k) dep[k] = depth_m<DK>(fb, pix[k], draw[k]);
+    // phase 3: depth / truncation test and distance (grid_fusion.py:278-286)
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        if (!__ballot(st[k] == 0.0f)) continue;
-        TSDF_DDIAG(3);
-        const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
-        const double z = fr.T[11] + fma(fr.T[10], pz, a2);
-        const double d = DK == 0 ? depth_m<DK>(fb, pix[k], draw[k]) : dep64[k];
-        diff[k] = d - z;
-        st[k] = st[k] != 0.0f ? st[k] : diff[k] < -trunc ? -1.0f : diff[k] < trunc ? 0.0f : 1.0f;
+        diff[k] = dep[k] - zc[k];
+        const bool dpos = DK == 0 ? draw[k] != 0u : dep[k] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
+        ok[k] = cand[k] & dpos & (diff[k] >= -trunc);
     }
 }
 
@@ -721,11 +714,17 @@ __device__ inline double dist_of(double trunc, double rtrunc, double diff) {
 // (listed by its z-low wave).
 constexpr int kResFree = -1, kResFail = -3;
 
-template <bool HASH, int DK, int CK, bool OW1, int NZ>
+// CU (u32 colour registers): the launch's volume is canonical (Vol::canon, host-checked), so every
+// colour the wave holds is an integer B*65536 + G*256 + R; it is held as that u32 between load and
+// store instead of as its f32, which the fast update decodes with byte conversions and encodes with
+// v_cvt_pk_u8_f32 (round to nearest even and clamp: the rint of the reference's blend, whose result
+// is <= 255) -- four VALU instructions fewer per step pair than through the f32.
+template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU = false>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, ListEntry entry, int zoff,
                                        unsigned long long* s_stat, const double* s_rcp,
                                        unsigned& nupd, unsigned& nuniq, int* res = nullptr) {
+    static_assert(!CU || (CK == 0 && OW1), "u32 colour registers: RGB8 frames, obs_weight 1");
     // nupd: the wave's voxel updates, accumulated over its items (scalar popcounts of the step
     // masks; integrate_list adds it to the statistics once per wave); nuniq: the voxels among them
     // updated at least once in the batch (popcounts of the OR of each step's masks over the frames)
@@ -738,7 +737,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     // opaque pointer, item_vol: its other fields are not held across the frame loop)
     const double trunc = v.trunc, rtrunc = v.rtrunc;
     const double* const rcp_hbm = v.rcp;
-    const bool canon = v.canon != 0;
+    const bool canon = CU || v.canon != 0;
     const int nb12 = v.nb[1] * v.nb[2];
     if (b >= v.nb[0] * nb12) {  // never for a list k_cull wrote; guards the pool against bad input
         if (lane == 0) atomicAdd(&s_stat[ST_BAD_ENTRY], 1ull);
@@ -762,11 +761,6 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     double pzs[kPz];
 #pragma unroll
     for (int k = 0; k < kPz; ++k) pzs[k] = readlane_f64(pz_l, k + zoff);
-    // the f32 filter's steps from the part's first (exact in f32); 8-step parts take them per frame
-    float dz[NZ];
-#pragma unroll
-    for (int k = 0; k < NZ; ++k)  // (wave-uniform: scalar registers)
-        dz[k] = NZ < 8 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)(pzs[k % kPz] - pzs[0])))) : 0.0f;
 
     // the brick's storage: dense brick b, or its hash pool block (wave-uniform; 32-bit for the hash,
     // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
@@ -823,16 +817,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #endif
         unsigned cpx[NZ];
         double diff[NZ];
-        float stv[NZ];  // -1: no update, 0: an update in the band (diff exact), 1: in free space
-        if constexpr (NZ == 8) {  // (8-step parts: the steps read out of the lanes per frame)
-            const double p0 = readlane_f64(pz_l, zoff);
-#pragma unroll
-            for (int k = 1; k < NZ; ++k) dz[k] = (float)(readlane_f64(pz_l, k + zoff) - p0);
-        }
-        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, dz, zoff, col_in, nz, cpx, diff, stv);
         bool okv[NZ];
-#pragma unroll
-        for (int k = 0; k < NZ; ++k) okv[k] = stv[k] >= 0.0f;
+        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
         bool need[kH];
 #pragma unroll
         for (int h = 0; h < kH; ++h) need[h] = okv[4 * h] | okv[4 * h + 1] | okv[4 * h + 2] | okv[4 * h + 3];
@@ -898,7 +884,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     c_canon = c_canon && canon_color(C.x) && canon_color(C.y) && canon_color(C.z) && canon_color(C.w);
                 }
                 ts[4 * h + 0] = T.x; ts[4 * h + 1] = T.y; ts[4 * h + 2] = T.z; ts[4 * h + 3] = T.w;
-                cs[4 * h + 0] = C.x; cs[4 * h + 1] = C.y; cs[4 * h + 2] = C.z; cs[4 * h + 3] = C.w;
+                if (CU) {
+                    cs[4 * h + 0] = __uint_as_float((unsigned)C.x); cs[4 * h + 1] = __uint_as_float((unsigned)C.y);
+                    cs[4 * h + 2] = __uint_as_float((unsigned)C.z); cs[4 * h + 3] = __uint_as_float((unsigned)C.w);
+                } else {
+                    cs[4 * h + 0] = C.x; cs[4 * h + 1] = C.y; cs[4 * h + 2] = C.z; cs[4 * h + 3] = C.w;
+                }
             }
             // Fast paths (wave-uniform; weights grow by one per frame, so the limits leave room
             // for a whole batch): every lane's weights are small integers -> RN(1/wn) from the LDS
@@ -922,7 +913,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
         float wnv[NZ], tqv[NZ], cnv[NZ];  // the step's new weight, tsdf and colour (if it updates)
-        if (!fast_c) TSDF_DDIAG(7);
+        if (!fast_c) TSDF_DDIAG(5);
         if (fast_c) {
             // Steps in pairs (k, k+1) on the packed f32 ALU (v_pk_*: two lanes' worth per
             // instruction): w + 1, w * t, the table offset 8 * (w + 1), and the colour channels'
@@ -934,14 +925,21 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             // Free space (wave-uniform): every updating voxel is at least trunc in front of the
             // surface (dist = min(1, diff / trunc) = 1 exactly) and still holds tsdf 1, so its new
             // tsdf is (w * 1 + 1) / (w + 1) = 1 exactly: the distance and tsdf quotients are skipped
-            // (an updating step that is not near has depth - z >= trunc: dist = 1, project_part)
             bool busy = false;
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) busy |= (stv[k] == 0.0f) | ((stv[k] > 0.0f) & (ts[k] != 1.0f));
+            for (int k = 0; k < NZ; ++k) busy |= okv[k] & ((diff[k] < trunc) | (ts[k] != 1.0f));
             const bool free_space = __ballot(busy) == 0;
-            if (free_space) TSDF_DDIAG(5);
+            if (free_space) TSDF_DDIAG(4);
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
+#if TSDF_PAIR_SKIP
+                if (__ballot(okv[k] | okv[k + 1]) == 0) {  // no lane updates either step: nothing to compute
+                    wnv[k] = ws[k], wnv[k + 1] = ws[k + 1];
+                    tqv[k] = ts[k], tqv[k + 1] = ts[k + 1];
+                    cnv[k] = cs[k], cnv[k + 1] = cs[k + 1];
+                    continue;
+                }
+#endif
                 const f2 w2 = {ws[k], ws[k + 1]};
                 const f2 a8 = pk_fma(w2, f2{8.0f, 8.0f}, f2{8.0f, 8.0f});  // byte offsets 8 * (w + 1)
                 const unsigned o0 = (unsigned)a8.x, o1 = (unsigned)a8.y;
@@ -965,12 +963,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        double dist = 1.0;
-                        if (__ballot(stv[k + j] == 0.0f)) {
-                            TSDF_DDIAG(6);
-                            dist = stv[k + j] == 0.0f ? dist_of(trunc, rtrunc, diff[k + j]) : 1.0;
-                        }
-                        const double num = (double)wt2[j] + dist;
+                        const double num = (double)wt2[j] + dist_of(trunc, rtrunc, diff[k + j]);
                         tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
                         r2[j] = (float)y[j];
                     }
@@ -978,21 +971,30 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 // colour (grid_fusion.py:302-314): float32, round half to even; decoded by bytes
                 // (v_cvt_f32_ubyte{0,1,2}), exact integer numerators by FMA, Markstein quotients;
                 // the average is <= 255, so min(255, .) is a no-op
-                const unsigned c0 = (unsigned)cs[k], c1 = (unsigned)cs[k + 1];
+                const unsigned c0 = CU ? __float_as_uint(cs[k]) : (unsigned)cs[k];
+                const unsigned c1 = CU ? __float_as_uint(cs[k + 1]) : (unsigned)cs[k + 1];
                 const f2 ob = {(float)((c0 >> 16) & 0xFFu), (float)((c1 >> 16) & 0xFFu)};
                 const f2 nb = {(float)((cpx[k] >> 16) & 0xFFu), (float)((cpx[k + 1] >> 16) & 0xFFu)};
-                const f2 rb = rint2(div_rn32x2(pk_fma(w2, ob, nb), wn2, r2));
+                const f2 qb = div_rn32x2(pk_fma(w2, ob, nb), wn2, r2);
                 const f2 og = {(float)((c0 >> 8) & 0xFFu), (float)((c1 >> 8) & 0xFFu)};
                 const f2 ng = {(float)((cpx[k] >> 8) & 0xFFu), (float)((cpx[k + 1] >> 8) & 0xFFu)};
-                const f2 rg = rint2(div_rn32x2(pk_fma(w2, og, ng), wn2, r2));
+                const f2 qg = div_rn32x2(pk_fma(w2, og, ng), wn2, r2);
                 const f2 orr = {(float)(c0 & 0xFFu), (float)(c1 & 0xFFu)};
                 const f2 nr = {(float)(cpx[k] & 0xFFu), (float)(cpx[k + 1] & 0xFFu)};
-                const f2 rr = rint2(div_rn32x2(pk_fma(w2, orr, nr), wn2, r2));
-                const f2 cn2 = pk_fma(rb, f2{65536.0f, 65536.0f}, pk_fma(rg, f2{256.0f, 256.0f}, rr));
+                const f2 qr = div_rn32x2(pk_fma(w2, orr, nr), wn2, r2);
                 wnv[k] = wn2.x;
                 wnv[k + 1] = wn2.y;
-                cnv[k] = cn2.x;
-                cnv[k + 1] = cn2.y;
+                if (CU) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        cnv[k + j] = __uint_as_float(__builtin_amdgcn_cvt_pk_u8_f32(
+                            qb[j], 2, __builtin_amdgcn_cvt_pk_u8_f32(qg[j], 1, __builtin_amdgcn_cvt_pk_u8_f32(qr[j], 0, 0u))));
+                } else {
+                    const f2 rb = rint2(qb), rg = rint2(qg), rr = rint2(qr);
+                    const f2 cn2 = pk_fma(rb, f2{65536.0f, 65536.0f}, pk_fma(rg, f2{256.0f, 256.0f}, rr));
+                    cnv[k] = cn2.x;
+                    cnv[k + 1] = cn2.y;
+                }
             }
         } else {
             // the exact paths: non-canonical colours or weights (table quotients where the weights
@@ -1001,7 +1003,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             for (int k = 0; k < NZ; ++k) {
                 const float w_old = ws[k];
                 const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
-                const double dist = stv[k] == 0.0f ? dist_of(trunc, rtrunc, diff[k]) : 1.0;
+                const double dist = dist_of(trunc, rtrunc, diff[k]);
                 const double num = (double)(w_old * ts[k]) + (OW1 ? dist : fr.ow * dist);
                 if (fast_t) tqv[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
                 else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, rcp_hbm[(int)wn]);
@@ -1019,22 +1021,22 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     ng = floorf((nc - nb * 65536.0f) / 256.0f);
                     nr = nc - nb * 65536.0f - ng * 256.0f;
                 }
-                const float co = cs[k];
+                const float co = CU ? (float)__float_as_uint(cs[k]) : cs[k];
                 const float ob = floorf(co / 65536.0f);
                 const float og = floorf((co - ob * 65536.0f) / 256.0f);
                 const float orr = co - ob * 65536.0f - og * 256.0f;
                 const float cb = fminf(255.0f, rintf((w_old * ob + (OW1 ? nb : fr.ow32 * nb)) / wn));
                 const float cg = fminf(255.0f, rintf((w_old * og + (OW1 ? ng : fr.ow32 * ng)) / wn));
                 const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
-                cnv[k] = cb * 65536.0f + cg * 256.0f + cr;
+                cnv[k] = CU ? __uint_as_float((unsigned)(cb * 65536.0f + cg * 256.0f + cr))
+                            : cb * 65536.0f + cg * 256.0f + cr;
             }
         }
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            const bool up = stv[k] >= 0.0f;  // (recomputed here: okv does not live across the update)
-            ws[k] = up ? wnv[k] : ws[k];
-            ts[k] = up ? tqv[k] : ts[k];
-            cs[k] = up ? cnv[k] : cs[k];
+            ws[k] = okv[k] ? wnv[k] : ws[k];
+            ts[k] = okv[k] ? tqv[k] : ts[k];
+            cs[k] = okv[k] ? cnv[k] : cs[k];
         }
     }
 #ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
@@ -1061,7 +1063,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         if (!loaded[h]) continue;
         *(float4*)(pool.weight + base + 4 * h) = make_float4(ws[4 * h], ws[4 * h + 1], ws[4 * h + 2], ws[4 * h + 3]);
         *(float4*)(pool.tsdf + base + 4 * h) = make_float4(ts[4 * h], ts[4 * h + 1], ts[4 * h + 2], ts[4 * h + 3]);
-        *(float4*)(pool.color + base + 4 * h) = make_float4(cs[4 * h], cs[4 * h + 1], cs[4 * h + 2], cs[4 * h + 3]);
+        if (CU)
+            *(float4*)(pool.color + base + 4 * h) =
+                make_float4((float)__float_as_uint(cs[4 * h]), (float)__float_as_uint(cs[4 * h + 1]),
+                            (float)__float_as_uint(cs[4 * h + 2]), (float)__float_as_uint(cs[4 * h + 3]));
+        else
+            *(float4*)(pool.color + base + 4 * h) = make_float4(cs[4 * h], cs[4 * h + 1], cs[4 * h + 2], cs[4 * h + 3]);
     }
     if constexpr (HASH) {  // voxel-entry bits: word z, bit (x*8+y); this wave owns words zoff .. zoff+NZ-1
         unsigned long long mine = 0;
@@ -1321,37 +1328,38 @@ typedef const __attribute__((address_space(4))) Vol* VolP;
 // copy), so its fields are not hoisted out of the item loop and held across it.
 __device__ inline const Vol& item_vol(const Vol& v) { return *(const Vol*)opaque((VolP)&v); }
 
-template <bool HASH, int DK, int CK, bool OW1, int NZ>
+template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU>
 __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq);
-template <bool HASH, int DK, int CK, bool OW1, int NZ>
+                                       unsigned& nuniq, unsigned* gq);
+template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU = false>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
+                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr,
+                                      unsigned* gq = nullptr) {
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
     unsigned nupd = 0, nuniq = 0;  // the wave's voxel updates over all its items (ST_VOXELS, ST_UNIQUE; wave-uniform)
-    integrate_items<HASH, DK, CK, OW1, NZ>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
-                                           s_next, wg, n_wg, res, nupd, nuniq);
+    integrate_items<HASH, DK, CK, OW1, NZ, CU>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
+                                           s_next, wg, n_wg, res, nupd, nuniq, gq);
     if (lane_id() == 0 && nupd) {
         atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
         atomicAdd(&s_stat[ST_UNIQUE], (unsigned long long)nuniq);
     }
 }
 
-template <bool HASH, int DK, int CK, bool OW1, int NZ>
+template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU>
 __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq) {
+                                       unsigned& nuniq, unsigned* gq) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[e / parts], (e % parts) * NZ,
+            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, list[e / parts], (e % parts) * NZ,
                                                    s_stat, s_rcp, nupd, nuniq);
         return;
     }
@@ -1388,9 +1396,22 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // brick of the list, spread over the whole image.  Renumbered, workgroup w deals as
         // (w % 8) * n_wg/8 + w / 8: each XCD takes runs of n_wg/8 consecutive bricks (neighbours
         // in the cull's order), whose gathers share its L2.
+        const int wg_hw = wg;
         if ((n_wg & 7) == 0) wg = (wg & 7) * (n_wg >> 3) + (wg >> 3);
 #endif
-        const unsigned mine = total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
+        // gq (fused launches, TSDF_GLOBAL_TAKE): the same XCD runs, but taken dynamically by every
+        // wave of the XCD from its queue gq[x] (then from the other XCDs' queues), so that the
+        // launch ends when the chip's last item does rather than its slowest workgroup's share
+        // (a shard's launch: ~35 items per workgroup, and workgroups sharing a CU run unevenly)
+        [[maybe_unused]] const bool split = (n_wg & 7) == 0;
+        [[maybe_unused]] const unsigned run = split ? (unsigned)(n_wg >> 3) : (unsigned)n_wg;
+#if TSDF_XCD_DEAL
+        [[maybe_unused]] int xq = split ? (wg_hw & 7) : 0;
+#else
+        [[maybe_unused]] int xq = split ? (wg & 7) : 0;
+#endif
+        [[maybe_unused]] int tried = 0;
+        const unsigned mine = gq ? 0u : total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
         const bool use_prio = kPrio && mine >= (HASH ? TSDF_PRIO_MIN_HASH : TSDF_PRIO_MIN);  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
         if (use_prio) __builtin_amdgcn_s_setprio(3);
@@ -1398,6 +1419,31 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // entry, before it integrates the current one -- one item held in reserve per wave)
         const auto take = [&](ListEntry& e, int& zoff) -> bool {
             unsigned j = 0;
+            if (gq) {
+                for (;;) {
+                    if (lane_id() == 0) j = atomicAdd(gq + xq, 1u);
+                    j = __builtin_amdgcn_readfirstlane(j);
+                    const unsigned i = j / parts;
+                    const long long k = (long long)(i / run) * n_wg + (long long)xq * run + (i % run);
+                    if (k < (long long)total) {
+                        if ((unsigned)k < k0) {  // (a stolen item: walk the classes from the top again)
+                            c = kMaxBatch - 1;
+                            k0 = 0;
+                            nc = min(coh_load(&count[c + 1]), nbk);
+                        }
+                        while (c > 0 && (unsigned)k - k0 >= nc) {
+                            k0 += nc;
+                            --c;
+                            nc = min(coh_load(&count[c + 1]), nbk);
+                        }
+                        e = list[(size_t)c * nbk + ((unsigned)k - k0)];
+                        zoff = (int)(j % parts) * NZ;
+                        return true;
+                    }
+                    if (!split || ++tried == 8) return false;
+                    xq = (xq + 1) & 7;  // this XCD's queue is empty: take from the next one's
+                }
+            }
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
             if (use_prio) {
@@ -1433,14 +1479,14 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             int zn = 0;
             const bool more = take(en, zn);
             // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
+            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
             have = more;
             e = en;
             zoff = zn;
         }
 #else
         while (take(e, zoff))  // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
+            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
 #endif
         if (use_prio) __builtin_amdgcn_s_setprio(0);
         return;
@@ -1452,7 +1498,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             --c;
             nc = min(coh_load(&count[c + 1]), nbk);
         }
-        integrate_brick<HASH, DK, CK, OW1, NZ>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
+        integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
                                                (e % parts) * NZ, s_stat, s_rcp, nupd, nuniq, res);
     }
 }
@@ -1689,7 +1735,7 @@ struct FusedArgs {
 };
 typedef const __attribute__((address_space(4))) FusedArgs* FusedArgsP;
 
-template <bool OW1, int NZ, int DK = 0>
+template <bool OW1, int NZ, int DK = 0, bool CU = false>
 __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_DENSE_WAVES))) void k_fused(FusedArgs a) {
     const FusedArgsP A = (FusedArgsP)__builtin_amdgcn_kernarg_segment_ptr();
     const Vol& v = *(const Vol*)opaque(&A->v);
@@ -1715,9 +1761,10 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
             for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedWG / 64;
-        integrate_list<false, DK, 0, OW1, NZ>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
+        integrate_list<false, DK, 0, OW1, NZ, CU>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
-                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
+                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi, nullptr,
+                                             TSDF_GLOBAL_TAKE ? sg.count_i + kQueueWord : nullptr);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
@@ -1784,7 +1831,7 @@ struct FusedHashArgs {
     Stage sg;
 };
 
-template <int DK = 0>
+template <int DK = 0, bool CU = false>
 __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TSDF_FUSED_HASH_WAVES))) void k_fused_hash(
         FusedHashArgs a) {
     typedef const __attribute__((address_space(4))) FusedHashArgs* ArgsP;
@@ -1810,8 +1857,9 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         for (int i = tid; i < kRcpTab / 2; i += kFusedHashWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedHashWG / 64;
-        integrate_list<true, DK, 0, true, 4>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
-                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i);
+        integrate_list<true, DK, 0, true, 4, CU>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
+                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i,
+                                            TSDF_GLOBAL_TAKE ? sg.count_i + kQueueWord : nullptr);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {

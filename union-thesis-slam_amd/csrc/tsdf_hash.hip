@@ -1000,10 +1000,15 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
         const FusedHashArgs args{B.vol, bi, bc, bp, B.pool, h->t, B.stats, sg};
-        if (dk == TSDF_DEPTH_U16_MM)
-            hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
-        else
-            hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+        // (u32 colour registers where the table's blocks are canonical, tsdf_device.h)
+        const bool cu = TSDF_COLOR_U32 && B.vol.canon;
+        if (dk == TSDF_DEPTH_U16_MM) {
+            if (cu) hipLaunchKernelGGL((k_fused_hash<0, true>), dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+            else hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+        } else {
+            if (cu) hipLaunchKernelGGL((k_fused_hash<1, true>), dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+            else hipLaunchKernelGGL(k_fused_hash<1>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+        }
         TSDF_HIP(hipGetLastError());
         if (!has_i) continue;
         TSDF_TRY(B.prof.end(B.stream, e0));
@@ -1142,9 +1147,11 @@ int hash_flush(tsdf_hash* h, bool wait = true) {
     const Base::Deferred d = B.dfr;
     B.dfr.n = 0;
     B.prestaged = d.slot;
+    B.pre_copied = d.copied;
     const int r = hash_run(h, d.n, B.hst_depth[d.slot], d.dk, B.hst_color[d.slot], d.ck, d.H, d.W, d.K, d.T,
                            wait ? 0 : kCheckLater);
     B.prestaged = -1;
+    B.pre_copied = 0;
     TSDF_TRY(r);
     if (wait) TSDF_TRY(hash_settle(h));
     return TSDF_OK;

@@ -124,12 +124,14 @@ struct Base {
     // asynchronous batch -- temporal batching for per-frame callers, same results.
     struct Deferred {
         int n = 0, H = 0, W = 0, dk = 0, ck = 0, slot = -1;
+        int copied = 0;  // frames whose DMA to the device staging slot is already issued
         double K[9];
         double T[16 * kMaxBatch];
         double ow[kMaxBatch];
     } dfr;
     int defer_next = 0;   // bounce slot of the next deferred batch
     int prestaged = -1;   // >= 0: the call's (single) batch already sits in this bounce slot
+    int pre_copied = 0;   // ... and its first pre_copied frames are already on their way to the device
     bool defer_same(int dk, int ck, int H, int W, const double* K) const;
     int defer_push(const void* depth, int dk, const void* color, int ck, int H, int W,
                    const double* K, const double* T, double ow);
