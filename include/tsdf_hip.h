@@ -72,8 +72,10 @@ typedef struct {
     int64_t lookups;          /* hash: block lookups performed */
     double kernel_ms;         /* integrate-kernel time from HIP events (profiling on only) */
     int64_t kernel_launches;  /* integrate-kernel launches timed */
-    int64_t bricks_skipped;   /* hash: bricks skipped for lack of table/pool space (must be 0
-                                 after a synchronous call; see tsdf_hash_integrate_batch) */
+    int64_t bricks_skipped;   /* hash: bricks a launch skipped for lack of table/pool space --
+                                 re-run exactly after growing by a synchronous call (and counted
+                                 here), reported as TSDF_E_CAPACITY by an asynchronous one; see
+                                 tsdf_hash_integrate_batch */
     int64_t list_errors;      /* brick-list entries out of range, dropped by the integrate kernel
                                  (always 0 unless device memory was corrupted) */
     int64_t batch_voxels;     /* sum over launches of U_batch: the voxels updated at least once by

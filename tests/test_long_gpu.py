@@ -177,7 +177,9 @@ def test_config4_rank_hash_shard_1024_extent_10000_frames(bench10k):
     1 cm; the reference loop is hash_demo1.py:114-125): shard 5 of 8 of a table created with 2^17
     slots (so the reference's 0.75 load-factor policy doubles it mid-run) and a pool of 2^14 blocks
     (grown ahead of the launches in flight), integrating 10,000 bench frames in one asynchronous
-    call.  No brick is skipped, the table doubled, and on two x rows a voxel is found iff its
+    call.  No brick is lost (the fresh table's first batch runs synchronously: the bricks its cull
+    found no room for are re-run exactly after the pool grows; every later, asynchronous launch
+    finds room, else sync() raises), the table doubled, and on two x rows a voxel is found iff its
     block's home bucket (in the table size of create) is in the shard's range and the dense grid
     updated it, with the dense grid's exact values; the dense rows equal the oracle bit for bit."""
     from tsdf_amd import grid_fusion, hash_fusion, scene, sharding
@@ -191,7 +193,7 @@ def test_config4_rank_hash_shard_1024_extent_10000_frames(bench10k):
     ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=False)
     ht.sync()  # (raises TSDF_E_CAPACITY if an asynchronous launch skipped a brick)
     info = ht.info()
-    assert ht.stats()["bricks_skipped"] == 0 and ht.stats()["list_errors"] == 0
+    assert ht.stats()["list_errors"] == 0
     assert info["capacity"] > 1 << 17 and info["used"] > 100_000 and info["pool_capacity"] > 1 << 14
     rows = [300, 700]
     orc = O.OracleTSDFVolume(bnds.copy(), 0.01, x_index=np.array(rows))

@@ -3,7 +3,10 @@ grid_demo1.py:76-87 / hash_demo1.py:114-125): the duration of every integrate() 
 the calls that only copy a frame into the deferred batch and the calls that also launch it
 (every TSDF_DEFER_FRAMES-th), for the dense volume and the hash table on the same frames.
 
-    PYTHONPATH=union-thesis-slam_amd python tools/gpu/dropin_trace.py [frames] [passes] [dense,hash]
+    PYTHONPATH=union-thesis-slam_amd python tools/gpu/dropin_trace.py [frames] [passes] [dense,hash] [grains]
+
+grains: comma-separated TSDF_DEFER_DMA_FRAMES values to compare (each handle reads it at create;
+8 = the whole batch's DMA at the flush, round 4's behaviour).
 
 Run it under `rocprofv3 --kernel-trace --stats` as well to set the GPU time per launched batch
 beside the host's time per batch.
@@ -33,6 +36,7 @@ def main():
     nd = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     passes = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     which = sys.argv[3].split(",") if len(sys.argv) > 3 else ["dense", "hash"]
+    grains = sys.argv[4].split(",") if len(sys.argv) > 4 else [None]
     per = int(os.environ.get("TSDF_DEFER_FRAMES", "8"))
     poses = scene.trajectory(nd, seed=0, radius_frac=scene.BENCH_RING)
     d, c = scene.render(poses, scene.make_spheres(0, ring_frac=scene.BENCH_RING), seed=0,
@@ -44,7 +48,9 @@ def main():
               "hash": lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
                                                     max_blocks=1 << 15)}
     out = {"frames": nd, "passes": passes, "defer_frames": per}
-    for name in which:
+    for grain, name in [(g, w) for g in grains for w in which]:
+        if grain is not None:
+            os.environ["TSDF_DEFER_DMA_FRAMES"] = grain
         v = makers[name]()
         v.integrate(ch[0], d64[0], K, poses[0])
         v.sync()
@@ -64,7 +70,7 @@ def main():
                         "final_sync_us": round((t_end - t1) * 1e6, 1), "copy_calls": stats(push),
                         "launch_calls": stats(launch),
                         "host_us_per_batch": round((sum(push) + sum(launch)) / (nd / per), 1)})
-        out[name] = res
+        out[name if grain is None else f"{name}_grain{grain}"] = res
         v.close()
     print(json.dumps(out))
 

@@ -39,5 +39,10 @@ int main() {
     run<8192>();
     run<12288>();
     run<16384>();
+    run<24576>();
+    run<32768>();
+    run<40960>();
+    run<49152>();
+    run<65536>();
     return 0;
 }

@@ -1,5 +1,5 @@
 """Where the time of an eighth-shard launch goes: per workgroup of the last fused launch of a call
-(integrate, cull and prep roles), its start, end and list items (diagnostic build: tools/build_variant.sh wgt
+(integrate, cull and prep roles), its start, end, list items and the CU it ran on (diagnostic build: tools/build_variant.sh wgt
 "-DTSDF_WG_TIMES", run with TSDF_HIP_LIB=abtest/libwgt.so).  Bench workload (scaling_sim's), one
 GPU and rank 0 of 2 / 4 / 8 cyclic column shards.  Prints one JSON line per configuration."""
 import ctypes
@@ -34,7 +34,7 @@ def main():
     fn = lib.tsdf_diag_wg_times
     fn.argtypes = [ctypes.c_void_p]
     NW = 16384
-    buf = np.zeros((3, NW), np.uint64)
+    buf = np.zeros((4, NW), np.uint64)
     for world in (1, 2, 4, 8):
         vol = grid_fusion.TSDFVolume(bnds.copy(), 0.02, shard=(0, world))
         rows = []
@@ -61,6 +61,11 @@ def main():
                 r[name] = [int(m.sum()), s[m].min(), s[m].max(), np.median(e[m]), e[m].max(), (e[m] - s[m]).mean()]
             r["items"] = it[role == 0]
             r["busy"] = (e - s)[role == 0]
+            # the CU each workgroup ran on: XCC id and HW_ID bits 8..15 (CU, SH, SE)
+            place = buf[3][keep]
+            cu = ((place >> np.uint64(32)) << np.uint64(8)) | ((place >> np.uint64(8)) & np.uint64(0xFF))
+            r["cu_i"] = cu[role == 0]
+            r["end_i"] = e[role == 0]
             rows.append(r)
         out = {"world": world, "span_us": round(float(np.mean([r["span"] for r in rows])), 2)}
         for name in ("integrate", "cull", "prep"):
@@ -75,6 +80,15 @@ def main():
         out["integrate"]["items_mean"] = round(float(it.mean()), 1)
         busy = rows[-1]["busy"]
         out["integrate"]["busy_deciles_last"] = [round(float(x), 1) for x in np.percentile(busy, range(0, 101, 10))]
+        # placement of the last launch's integrate workgroups: how many share a CU, their busy time
+        # by that count, and when each CU's last integrate workgroup ends
+        cu_i, end_i = rows[-1]["cu_i"], rows[-1]["end_i"]
+        ucu, inv, cnt = np.unique(cu_i, return_inverse=True, return_counts=True)
+        per = cnt[inv]
+        out["integrate"]["cus_by_wgs"] = {str(k): int((cnt == k).sum()) for k in np.unique(cnt)}
+        out["integrate"]["busy_by_wgs_per_cu"] = {str(k): round(float(busy[per == k].mean()), 1) for k in np.unique(per)}
+        cu_end = np.array([end_i[inv == j].max() for j in range(len(ucu))])
+        out["integrate"]["cu_end_deciles"] = [round(float(x), 1) for x in np.percentile(cu_end, range(0, 101, 10))]
         print(json.dumps(out), flush=True)
         del vol
 

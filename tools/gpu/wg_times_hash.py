@@ -62,7 +62,7 @@ def main():
     fns = {"dense": lib.tsdf_diag_wg_times, "hash": lib.tsdf_diag_wg_times_hash}
     for fn in fns.values():
         fn.argtypes = [ctypes.c_void_p]
-    buf = np.zeros((3, NW), np.uint64)
+    buf = np.zeros((4, NW), np.uint64)
 
     def run(kind, v, label):
         B = v.frames_per_launch()

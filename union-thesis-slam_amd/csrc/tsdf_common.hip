@@ -498,15 +498,18 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
     std::memcpy(dfr.T + 16 * i, T, 16 * sizeof(double));
     dfr.ow[i] = ow;
     dfr.n = i + 1;
-    if (dfr.n * 2 == defer_frames && dfr.n >= 2) {
-        // half the batch collected: its DMA starts now (one transfer per field), so that at the
-        // flush only the other half is still to cross PCIe before the batch's launches can run --
-        // the hash flush waits for the previous batch's pool report, i.e. for that batch's whole
-        // DMA + launches, which with one DMA per batch took longer than the host's copies of the
-        // next 8 frames (profiles/r05_dropin/)
-        TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[dfr.slot], 0));
-        TSDF_HIP(hipMemcpyAsync(st_depth[dfr.slot], hst_depth[dfr.slot], dbytes * dfr.n, hipMemcpyHostToDevice, cstream));
-        TSDF_HIP(hipMemcpyAsync(st_color[dfr.slot], hst_color[dfr.slot], cbytes * dfr.n, hipMemcpyHostToDevice, cstream));
+    if (dfr.n - dfr.copied >= dma_grain && dfr.n < defer_frames) {
+        // the batch's DMA runs as its frames arrive, dma_grain frames at a time (one transfer per
+        // field), so that at the flush at most dma_grain frames are still to cross PCIe before the
+        // batch's launches can run: the hash flush waits for the previous batch's pool report, i.e.
+        // for that batch's DMA and launches, which with one DMA per batch took longer than the
+        // host's copies of the next 8 frames (tools/gpu/dropin_trace.py, profiles/r05_dropin/)
+        if (dfr.copied == 0) TSDF_HIP(hipStreamWaitEvent(cstream, ev_free[dfr.slot], 0));
+        const size_t c0 = (size_t)dfr.copied, nc = (size_t)(dfr.n - dfr.copied);
+        TSDF_HIP(hipMemcpyAsync((char*)st_depth[dfr.slot] + dbytes * c0, (const char*)hst_depth[dfr.slot] + dbytes * c0,
+                                dbytes * nc, hipMemcpyHostToDevice, cstream));
+        TSDF_HIP(hipMemcpyAsync((char*)st_color[dfr.slot] + cbytes * c0, (const char*)hst_color[dfr.slot] + cbytes * c0,
+                                cbytes * nc, hipMemcpyHostToDevice, cstream));
         dfr.copied = dfr.n;
     }
     return TSDF_OK;

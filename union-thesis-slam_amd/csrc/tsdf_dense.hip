@@ -563,10 +563,10 @@ int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {
 
 #ifdef TSDF_WG_TIMES
 // (diagnostic builds) the last fused launch's per-workgroup start / end / role|items:
-// out[3 * kWgTimes]
+// out[4 * kWgTimes]
 extern "C" int tsdf_diag_wg_times(unsigned long long* out) {
     TSDF_HIP(hipDeviceSynchronize());
-    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 3 * kWgTimes));
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 4 * kWgTimes));
     return TSDF_OK;
 }
 #endif

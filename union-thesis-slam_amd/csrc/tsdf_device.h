@@ -95,7 +95,7 @@ struct PyrGeo {
 #define TSDF_MAX_BATCH 16
 #endif
 constexpr int kMaxBatch = TSDF_MAX_BATCH;
-static_assert(kMaxBatch == 8 || kMaxBatch == 16, "frames per batch: 8 or 16");
+static_assert(kMaxBatch == 8 || kMaxBatch == 16 || kMaxBatch == 32, "frames per batch: 8, 16 or 32");
 // Frames per launch of a whole (unsharded) volume; shards of a multi-GPU volume take kMaxBatch
 // (Base::set_batch): a shard's launch is short, and its fixed costs -- dispatch, the end of the
 // kernel, the cull / prep tail -- weigh more per frame.
@@ -111,20 +111,15 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_RCP_SHARE  // project_part: one reciprocal per four z-steps
-#define TSDF_RCP_SHARE 0
-#endif
-#ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU)
-#define TSDF_COLOR_U32 0
-#endif
-#ifndef TSDF_PAIR_SKIP  // fast update: skip step pairs that no lane of the wave updates
-#define TSDF_PAIR_SKIP 0
+#ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU;
+#define TSDF_COLOR_U32 1  // round 5: dense -1.5 %, hash -1.5 % time per launch, profiles/r05_ab/)
 #endif
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); words kDoneWord / kDoneWordC = integrate and cull workgroups finished (fused hash
 // launch; the launch counts on its cull's set, or on its integrate's set when it has no cull);
 // words kQueueWord .. +7 = the fused integrate's per-XCD item queues (TSDF_GLOBAL_TAKE).
-constexpr int kCountWords = 48, kDoneWord = 24, kDoneWordC = 25, kQueueWord = 32;
+constexpr int kDoneWord = kMaxBatch + 8, kDoneWordC = kMaxBatch + 9, kQueueWord = kMaxBatch + 16;
+constexpr int kCountWords = kQueueWord + 16;
 #ifndef TSDF_GLOBAL_TAKE  // fused launches: integrate items taken from per-XCD queues (integrate_items)
 #define TSDF_GLOBAL_TAKE 0
 #endif
@@ -609,25 +604,8 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         zc[k] = fr.T[11] + fma(fr.T[10], pz, a2);  // fma(T3, 1, s) == T3 + s
     }
     double rzs[NZ];
-#if TSDF_RCP_SHARE
-    // one v_rcp_f64 (10.5 issue cycles, four FMAs' worth) per four steps: r = rcp(z0 z1 z2 z3),
-    // 1/(z0 z1) = (z2 z3) r, 1/z0 = z1 / (z0 z1) ...  -- the rcp's 2^-24.4 relative error plus a few
-    // f64 roundings, inside the margin's 2^-24.3; a zero or non-finite z makes its group's
-    // quotients non-finite, which the boundary test sends to the exact path
-#pragma unroll
-    for (int k = 0; k < NZ; k += 4) {
-        const double z01 = zc[k] * zc[k + 1], z23 = zc[k + 2] * zc[k + 3];
-        const double r = __builtin_amdgcn_rcp(z01 * z23);
-        const double r01 = z23 * r, r23 = z01 * r;
-        rzs[k] = zc[k + 1] * r01;
-        rzs[k + 1] = zc[k] * r01;
-        rzs[k + 2] = zc[k + 3] * r23;
-        rzs[k + 3] = zc[k + 2] * r23;
-    }
-#else
 #pragma unroll
     for (int k = 0; k < NZ; ++k) rzs[k] = __builtin_amdgcn_rcp(zc[k]);  // v_rcp_f64, see frame_margin
-#endif
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
         const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
@@ -932,14 +910,6 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             if (free_space) TSDF_DDIAG(4);
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
-#if TSDF_PAIR_SKIP
-                if (__ballot(okv[k] | okv[k + 1]) == 0) {  // no lane updates either step: nothing to compute
-                    wnv[k] = ws[k], wnv[k + 1] = ws[k + 1];
-                    tqv[k] = ts[k], tqv[k + 1] = ts[k + 1];
-                    cnv[k] = cs[k], cnv[k + 1] = cs[k + 1];
-                    continue;
-                }
-#endif
                 const f2 w2 = {ws[k], ws[k + 1]};
                 const f2 a8 = pk_fma(w2, f2{8.0f, 8.0f}, f2{8.0f, 8.0f});  // byte offsets 8 * (w + 1)
                 const unsigned o0 = (unsigned)a8.x, o1 = (unsigned)a8.y;
@@ -1400,17 +1370,20 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         if ((n_wg & 7) == 0) wg = (wg & 7) * (n_wg >> 3) + (wg >> 3);
 #endif
         // gq (fused launches, TSDF_GLOBAL_TAKE): the same XCD runs, but taken dynamically by every
-        // wave of the XCD from its queue gq[x] (then from the other XCDs' queues), so that the
-        // launch ends when the chip's last item does rather than its slowest workgroup's share
-        // (a shard's launch: ~35 items per workgroup, and workgroups sharing a CU run unevenly)
+        // wave of the XCD from its queue gq[x], so that the launch ends when the XCD's last item
+        // does rather than its slowest workgroup's share (a shard's launch: ~35 items per
+        // workgroup, and workgroups sharing a CU run unevenly).  The queue's atomics are
+        // workgroup-scope: performed in the XCD's L2, which every workgroup of the XCD shares
+        // (an agent-scope atomic goes past the L2 and costs microseconds) -- so a
+        // queue is only ever taken from by the workgroups of one XCD (workgroup w on XCD w % 8).
         [[maybe_unused]] const bool split = (n_wg & 7) == 0;
+        if (!split) gq = nullptr;  // (the queues need whole XCD groups of workgroups)
         [[maybe_unused]] const unsigned run = split ? (unsigned)(n_wg >> 3) : (unsigned)n_wg;
 #if TSDF_XCD_DEAL
         [[maybe_unused]] int xq = split ? (wg_hw & 7) : 0;
 #else
         [[maybe_unused]] int xq = split ? (wg & 7) : 0;
 #endif
-        [[maybe_unused]] int tried = 0;
         const unsigned mine = gq ? 0u : total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
         const bool use_prio = kPrio && mine >= (HASH ? TSDF_PRIO_MIN_HASH : TSDF_PRIO_MIN);  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
@@ -1420,29 +1393,19 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         const auto take = [&](ListEntry& e, int& zoff) -> bool {
             unsigned j = 0;
             if (gq) {
-                for (;;) {
-                    if (lane_id() == 0) j = atomicAdd(gq + xq, 1u);
-                    j = __builtin_amdgcn_readfirstlane(j);
-                    const unsigned i = j / parts;
-                    const long long k = (long long)(i / run) * n_wg + (long long)xq * run + (i % run);
-                    if (k < (long long)total) {
-                        if ((unsigned)k < k0) {  // (a stolen item: walk the classes from the top again)
-                            c = kMaxBatch - 1;
-                            k0 = 0;
-                            nc = min(coh_load(&count[c + 1]), nbk);
-                        }
-                        while (c > 0 && (unsigned)k - k0 >= nc) {
-                            k0 += nc;
-                            --c;
-                            nc = min(coh_load(&count[c + 1]), nbk);
-                        }
-                        e = list[(size_t)c * nbk + ((unsigned)k - k0)];
-                        zoff = (int)(j % parts) * NZ;
-                        return true;
-                    }
-                    if (!split || ++tried == 8) return false;
-                    xq = (xq + 1) & 7;  // this XCD's queue is empty: take from the next one's
+                if (lane_id() == 0) j = __hip_atomic_fetch_add(gq + xq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                j = __builtin_amdgcn_readfirstlane(j);
+                const unsigned i = j / parts;
+                const long long k = (long long)(i / run) * n_wg + (long long)xq * run + (i % run);
+                if (k >= (long long)total) return false;
+                while (c > 0 && (unsigned)k - k0 >= nc) {
+                    k0 += nc;
+                    --c;
+                    nc = min(coh_load(&count[c + 1]), nbk);
                 }
+                e = list[(size_t)c * nbk + ((unsigned)k - k0)];
+                zoff = (int)(j % parts) * NZ;
+                return true;
             }
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
@@ -1723,7 +1686,13 @@ struct Stage {
 // start and end (s_memrealtime, 100 MHz) and role << 32 | the list items its waves took (role 0
 // integrate, 1 cull, 2 prep).
 constexpr int kWgTimes = 16384;
-__device__ unsigned long long g_wg_times[3][kWgTimes];
+__device__ unsigned long long g_wg_times[4][kWgTimes];  // start, end, role << 32 | items, XCC << 32 | HW_ID
+__device__ inline unsigned long long wg_place() {  // where the workgroup runs: XCC id << 32 | HW_ID (CU, SE, ...)
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return ((unsigned long long)xcc << 32) | hw;
+}
 #endif
 // The dense fused launch's arguments as one struct (the kernel addresses its kernarg copy).
 struct FusedArgs {
@@ -1780,6 +1749,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     __syncthreads();
     if (tid == 0 && rec) {
         g_wg_times[1][b] = __builtin_amdgcn_s_memrealtime();
+        g_wg_times[3][b] = wg_place();
         g_wg_times[2][b] = ((unsigned long long)(b < sg.gi ? 0 : b < sg.gi + sg.gc ? 1 : 2) << 32) |
                            (b < sg.gi ? s_next : 0u);
     }
@@ -1890,6 +1860,7 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
     __syncthreads();
     if (tid == 0 && rec) {
         g_wg_times[1][b] = __builtin_amdgcn_s_memrealtime();
+        g_wg_times[3][b] = wg_place();
         g_wg_times[2][b] = ((unsigned long long)(b < sg.gi ? 0 : b < sg.gi + sg.gc ? 1 : 2) << 32) |
                            (b < sg.gi ? s_next : 0u);
     }

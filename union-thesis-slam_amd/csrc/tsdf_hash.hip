@@ -1728,7 +1728,7 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 // (diagnostic builds) the last fused hash launch's per-workgroup start / end / role|items
 extern "C" int tsdf_diag_wg_times_hash(unsigned long long* out) {
     TSDF_HIP(hipDeviceSynchronize());
-    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 3 * kWgTimes));
+    TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 4 * kWgTimes));
     return TSDF_OK;
 }
 #endif

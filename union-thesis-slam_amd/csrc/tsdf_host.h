@@ -78,11 +78,14 @@ struct Base {
         defer_frames = batch < 8 ? batch : 8;
         if (const char* e = getenv("TSDF_DEFER_FRAMES")) defer_frames = atoi(e);
         defer_frames = defer_frames < 1 ? 1 : defer_frames > batch ? batch : defer_frames;
+        if (const char* e = getenv("TSDF_DEFER_DMA_FRAMES")) dma_grain = atoi(e) < 1 ? 1 : atoi(e);
     }
     // frames a deferred per-frame batch collects (TSDF_DEFER) before it runs: 8 -- the host's
     // frame copies of the next batch overlap the ingest and integrate of this one at a finer
     // grain than a whole launch's 16 frames (TSDF_DEFER_FRAMES overrides)
     int defer_frames = 8;
+    // deferred frames whose DMA is issued together while the batch fills (TSDF_DEFER_DMA_FRAMES)
+    int dma_grain = 2;
     // Per-batch buffers of the CURRENT buffer set (use_set).
     float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
     unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
