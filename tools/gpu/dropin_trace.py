@@ -11,6 +11,7 @@ grains: comma-separated TSDF_DEFER_DMA_FRAMES values to compare (each handle rea
 Run it under `rocprofv3 --kernel-trace --stats` as well to set the GPU time per launched batch
 beside the host's time per batch.
 """
+import ctypes
 import json
 import os
 import sys
@@ -21,7 +22,10 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                                 "union-thesis-slam_amd"))
-from tsdf_amd import grid_fusion, hash_fusion, scene  # noqa: E402
+from tsdf_amd import _ffi, grid_fusion, hash_fusion, scene  # noqa: E402
+
+HOST_PARTS = ["deferred_flushes_us", "report_wait_us", "prepare_batch_us", "launches_us", "call_end_us",
+              "flushes", "unused6", "other_flushes_us"]
 
 
 def stats(us):
@@ -48,6 +52,10 @@ def main():
               "hash": lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
                                                     max_blocks=1 << 15)}
     out = {"frames": nd, "passes": passes, "defer_frames": per}
+    # (a -DTSDF_DIAG build: the hash flush's host time by part, tsdf_diag_host_times)
+    lib = _ffi.load()
+    host_times = getattr(lib, "tsdf_diag_host_times", None) if hasattr(lib, "tsdf_diag_host_times") else None
+    buf = (ctypes.c_double * 8)()
     for grain, name in [(g, w) for g in grains for w in which]:
         if grain is not None:
             os.environ["TSDF_DEFER_DMA_FRAMES"] = grain
@@ -56,6 +64,8 @@ def main():
         v.sync()
         res = []
         for p in range(passes):
+            if host_times is not None:
+                host_times(buf)
             push, launch = [], []
             t_start = time.perf_counter()
             for i in range(nd):
@@ -70,6 +80,10 @@ def main():
                         "final_sync_us": round((t_end - t1) * 1e6, 1), "copy_calls": stats(push),
                         "launch_calls": stats(launch),
                         "host_us_per_batch": round((sum(push) + sum(launch)) / (nd / per), 1)})
+            if host_times is not None and name == "hash":
+                host_times(buf)
+                res[-1]["flush_parts_us_per_batch"] = {k: round(buf[i] / max(buf[5], 1.0), 1)
+                                                       for i, k in enumerate(HOST_PARTS) if i != 5}
         out[name if grain is None else f"{name}_grain{grain}"] = res
         v.close()
     print(json.dumps(out))

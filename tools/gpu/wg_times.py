@@ -46,7 +46,7 @@ def main():
                 continue
             fn(buf.ctypes.data)
             t0 = buf[0].astype(np.int64)
-            keep = (buf[1] != 0) & (t0 > t0.max() - 100000)  # this launch only (not an older, larger one)
+            keep = (buf[1] != 0) & (t0 > t0.max() - 1000000)  # this launch only (not an older, larger one; < 10 ms)
             t0 = t0[keep]
             t1 = buf[1][keep].astype(np.int64)
             role = (buf[2][keep] >> np.uint64(32)).astype(np.int64)
@@ -65,6 +65,10 @@ def main():
             place = buf[3][keep]
             cu = ((place >> np.uint64(32)) << np.uint64(8)) | ((place >> np.uint64(8)) & np.uint64(0xFF))
             r["cu_i"] = cu[role == 0]
+            # workgroup b on XCD b % 8 (the dispatch order XCD-aware dealing assumes)?
+            b_idx = np.nonzero(keep)[0]
+            xcc = (place >> np.uint64(32)).astype(np.int64)
+            r["xcc_rr"] = float(np.mean(xcc == (b_idx % 8)))
             r["end_i"] = e[role == 0]
             rows.append(r)
         out = {"world": world, "span_us": round(float(np.mean([r["span"] for r in rows])), 2)}
@@ -88,6 +92,7 @@ def main():
         out["integrate"]["cus_by_wgs"] = {str(k): int((cnt == k).sum()) for k in np.unique(cnt)}
         out["integrate"]["busy_by_wgs_per_cu"] = {str(k): round(float(busy[per == k].mean()), 1) for k in np.unique(per)}
         cu_end = np.array([end_i[inv == j].max() for j in range(len(ucu))])
+        out["xcc_is_wg_mod_8"] = round(float(np.mean([r["xcc_rr"] for r in rows])), 4)
         out["integrate"]["cu_end_deciles"] = [round(float(x), 1) for x in np.percentile(cu_end, range(0, 101, 10))]
         print(json.dumps(out), flush=True)
         del vol

@@ -17,6 +17,24 @@
 
 #include "tsdf_host.h"
 
+#ifdef TSDF_DIAG
+// (diagnostic builds, tools/gpu/dropin_trace.py) host time of the hash drop-in's flush, by part:
+// 0 whole deferred flushes, 1 waiting for a pool report, 2 prepare_batch, 3 kernel launches,
+// 4 the call's end (k_free_unused), 5 flushes counted
+static double g_host_us[8];
+struct HostTimer {
+    int slot;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit HostTimer(int s) : slot(s) {}
+    ~HostTimer() {
+        g_host_us[slot] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+#define TSDF_HOST_TIME(slot) HostTimer tsdf_host_timer_##slot(slot)
+#else
+#define TSDF_HOST_TIME(slot) ((void)0)
+#endif
+
 using namespace tsdf;
 
 // A growable device array on the virtual-memory API: the address range for the largest size
@@ -801,6 +819,7 @@ int take_overflow(tsdf_hash* h) {
 
 // Report of allocating launch s (written by its committing thread; waits for it).
 int wait_report(tsdf_hash* h, long long s, PoolReport* out) {
+    TSDF_HOST_TIME(1);
     volatile PoolReport* r = h->h_rb + (s % kReports);
     for (int spin = 0;; ++spin) {
         if (__atomic_load_n(&r->seq, __ATOMIC_ACQUIRE) == s + 1) break;
@@ -955,6 +974,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
             const int n = n_frames - f0 < nbat ? n_frames - f0 : nbat;
             B.use_set(set_of(jp));
             // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1.
+            TSDF_HOST_TIME(2);
             TSDF_TRY(B.prepare_batch(&bts[jp % kSets], depth, dk, color, TSDF_COLOR_RGB8, H, W,
                                      K, Tinv, nullptr, 1.0, flags, f0, n, jp % kSlots));
         }
@@ -1000,6 +1020,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         hipEvent_t e0 = nullptr;
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
         const FusedHashArgs args{B.vol, bi, bc, bp, B.pool, h->t, B.stats, sg};
+        TSDF_HOST_TIME(3);
         // (u32 colour registers where the table's blocks are canonical, tsdf_device.h)
         const bool cu = TSDF_COLOR_U32 && B.vol.canon;
         if (dk == TSDF_DEPTH_U16_MM) {
@@ -1030,6 +1051,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     }
     // the blocks the call's culls inserted that no frame gave an entry (after the last launch, which
     // has no cull: no claim word is pending)
+    TSDF_HOST_TIME(4);
     hipLaunchKernelGGL(k_free_unused, dim3(256), dim3(256), 0, B.stream, B.vol, h->t);
     TSDF_HIP(hipGetLastError());
     TSDF_HIP(hipMemsetAsync(&h->t.st->n_inserted, 0, sizeof(long long), B.stream));
@@ -1140,6 +1162,10 @@ int hash_settle(tsdf_hash* h) {
 // bricks re-run exactly before any later frame is integrated.
 int hash_flush(tsdf_hash* h, bool wait = true) {
     Base& B = h->b;
+#ifdef TSDF_DIAG
+    if (!wait && B.dfr.n) g_host_us[5] += 1.0;
+    HostTimer whole(wait || !B.dfr.n ? 7 : 0);
+#endif
     // (wait = false: a pending batch is settled inside hash_run, right before this batch's
     // integrate launch, once this batch's ingest / prep / cull are queued behind it)
     if (wait || B.dfr.n == 0) TSDF_TRY(hash_settle(h));
@@ -1729,6 +1755,17 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 extern "C" int tsdf_diag_wg_times_hash(unsigned long long* out) {
     TSDF_HIP(hipDeviceSynchronize());
     TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 4 * kWgTimes));
+    return TSDF_OK;
+}
+#endif
+
+#ifdef TSDF_DIAG
+// (diagnostic builds) the drop-in flush's host times (g_host_us above), read and cleared
+extern "C" int tsdf_diag_host_times(double* out) {
+    for (int i = 0; i < 8; ++i) {
+        out[i] = g_host_us[i];
+        g_host_us[i] = 0.0;
+    }
     return TSDF_OK;
 }
 #endif
