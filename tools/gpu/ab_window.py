@@ -1,6 +1,7 @@
 """A/B probe of one library build (TSDF_HIP_LIB selects it) at the driver's own window: a fresh
 volume, 5 untimed batches, 20 timed batches (bench.py --steps 20 --warmup 5), repeated; dense and
-hash; plus the 250-step default window once.  One JSON line.
+hash; plus the 250-step default window once, and frames 160-799 of a fresh volume (the same
+frames whatever the build's frames per launch).  One JSON line.
 
     PYTHONPATH=union-thesis-slam_amd python tools/gpu/ab_window.py [reps] [name]
 """
@@ -71,6 +72,16 @@ def main():
     run(vol, 0, 12 * B, False, sync=False)
     r = run(vol, 12 * B, 250 * B, True, sync=False)
     out["dense_250_fps"], out["dense_250_us"] = round(r[0], 1), round(r[1], 2)
+    # the same frames whatever the launch size (160 untimed, then 640 timed: builds with 16- and
+    # 32-frame launches compare on equal work), kernel time per frame
+    rows = []
+    for _ in range(reps):
+        vol.reset()
+        run(vol, 0, 160, False, sync=False)
+        f, us, _ = run(vol, 160, 640, True, sync=False)
+        rows.append((f, us / B))
+    out["dense_fixed_fps"] = round(statistics.median(r[0] for r in rows), 1)
+    out["dense_fixed_us_per_frame"] = round(statistics.median(r[1] for r in rows), 3)
     vol.close()
     rows = []
     for _ in range(reps):
@@ -89,6 +100,15 @@ def main():
     r = run(ht, 12 * B, 250 * B, True, sync=False)
     out["hash_250_fps"], out["hash_250_us"] = round(r[0], 1), round(r[1], 2)
     ht.close()
+    rows = []
+    for _ in range(reps):
+        ht = hash_fusion.HashTable(bnds.copy(), 0.02, 1 << 22, max_blocks=1 << 15)
+        run(ht, 0, 160, False, sync=True)
+        f, us, _ = run(ht, 160, 640, True, sync=False)
+        rows.append((f, us / B))
+        ht.close()
+    out["hash_fixed_fps"] = round(statistics.median(r[0] for r in rows), 1)
+    out["hash_fixed_us_per_frame"] = round(statistics.median(r[1] for r in rows), 3)
     print(json.dumps(out), flush=True)
 
 

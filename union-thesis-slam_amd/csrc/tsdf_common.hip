@@ -164,10 +164,6 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
         TSDF_HIP(hipEventRecord(ev_copied[k], cstream));
     }
     TSDF_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    TSDF_HIP(hipMalloc(&list_set[0], sizeof(ListEntry) * (size_t)n_bricks * kMaxBatch));
-    TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
-    TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * kCountWords, stream));
-    use_set(0);
     TSDF_HIP(hipMalloc(&rcp, sizeof(double) * kRcpBig));
     hipLaunchKernelGGL(k_fill_rcp, dim3((kRcpBig + 255) / 256), dim3(256), 0, stream, rcp);
     TSDF_HIP(hipGetLastError());
@@ -177,12 +173,30 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     return TSDF_OK;
 }
 
+// Frames per launch (the create functions call it once, after init): sizes the per-batch buffers,
+// whose frame and cost-class dimension is the handle's batch -- 16 for a whole volume, 32 for a
+// shard -- not the kernels' capacity kMaxBatch; then buffer set 0's list and counters.
+int Base::set_batch(int want) {
+    if (const char* e = getenv("TSDF_BATCH")) want = atoi(e);
+    batch = want < 1 ? 1 : want > kMaxBatch ? kMaxBatch : want;
+    defer_frames = batch < 8 ? batch : 8;
+    if (const char* e = getenv("TSDF_DEFER_FRAMES")) defer_frames = atoi(e);
+    defer_frames = defer_frames < 1 ? 1 : defer_frames > batch ? batch : defer_frames;
+    if (const char* e = getenv("TSDF_DEFER_DMA_FRAMES")) dma_grain = atoi(e) < 1 ? 1 : atoi(e);
+    if (list_set[0]) return TSDF_OK;
+    TSDF_HIP(hipMalloc(&list_set[0], sizeof(ListEntry) * (size_t)n_bricks * batch));
+    TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
+    TSDF_HIP(hipMemsetAsync(count_set[0], 0, sizeof(unsigned int) * kCountWords, stream));
+    use_set(0);
+    return TSDF_OK;
+}
+
 // Buffer sets 1..n-1 (lists and counters now; pyramids, RGBX and masks when a batch needs them).
 int Base::use_sets(int n) {
     if (n <= n_sets) return TSDF_OK;
     TSDF_TRY(sync_all());
     for (int k = n_sets; k < n; ++k) {
-        TSDF_HIP(hipMalloc(&list_set[k], sizeof(ListEntry) * (size_t)n_bricks * kMaxBatch));
+        TSDF_HIP(hipMalloc(&list_set[k], sizeof(ListEntry) * (size_t)n_bricks * batch));
         TSDF_HIP(hipMalloc(&count_set[k], sizeof(unsigned int) * kCountWords));
         TSDF_HIP(hipMemsetAsync(count_set[k], 0, sizeof(unsigned int) * kCountWords, stream));
     }
@@ -209,8 +223,8 @@ int Base::ensure_pyr(int H, int W) {
     }
     lay = pyr_layout(H, W);
     for (int k = 0; k < n_sets; ++k) {
-        TSDF_HIP(hipMalloc(&pyr_set[k], sizeof(float) * (size_t)lay.total * kMaxBatch));
-        TSDF_HIP(hipMalloc(&rgbx_set[k], sizeof(unsigned) * (size_t)H * W * kMaxBatch));
+        TSDF_HIP(hipMalloc(&pyr_set[k], sizeof(float) * (size_t)lay.total * batch));
+        TSDF_HIP(hipMalloc(&rgbx_set[k], sizeof(unsigned) * (size_t)H * W * batch));
     }
     pyr_H = H;
     pyr_W = W;
@@ -398,7 +412,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
             dmask_set[k] = nullptr;
         }
         for (int k = 0; k < n_sets; ++k)
-            TSDF_HIP(hipMalloc(&dmask_set[k], sizeof(unsigned short) * npx * kMaxBatch));
+            TSDF_HIP(hipMalloc(&dmask_set[k], sizeof(unsigned short) * npx * batch));
         dmask_px = npx;
     }
     use_set(cur_set);  // (re)read the set's pointers: the buffers above may be new
@@ -452,7 +466,7 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
 }
 
 int Base::stage_alloc(size_t dbytes, size_t cbytes) {
-    if (st_depth_bytes >= dbytes * kMaxBatch && st_color_bytes >= cbytes * kMaxBatch) return TSDF_OK;
+    if (st_depth_bytes >= dbytes * batch && st_color_bytes >= cbytes * batch) return TSDF_OK;
     TSDF_TRY(sync_all());
     for (int k = 0; k < kSlots; ++k) {
         if (st_depth[k]) TSDF_HIP(hipFree(st_depth[k]));
@@ -463,13 +477,13 @@ int Base::stage_alloc(size_t dbytes, size_t cbytes) {
     }
     st_depth_bytes = st_color_bytes = 0;
     for (int k = 0; k < kSlots; ++k) {
-        TSDF_HIP(hipMalloc(&st_depth[k], dbytes * kMaxBatch));
-        TSDF_HIP(hipMalloc(&st_color[k], cbytes * kMaxBatch));
-        TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * kMaxBatch, hipHostMallocDefault));
-        TSDF_HIP(hipHostMalloc(&hst_color[k], cbytes * kMaxBatch, hipHostMallocDefault));
+        TSDF_HIP(hipMalloc(&st_depth[k], dbytes * batch));
+        TSDF_HIP(hipMalloc(&st_color[k], cbytes * batch));
+        TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * batch, hipHostMallocDefault));
+        TSDF_HIP(hipHostMalloc(&hst_color[k], cbytes * batch, hipHostMallocDefault));
     }
-    st_depth_bytes = dbytes * kMaxBatch;
-    st_color_bytes = cbytes * kMaxBatch;
+    st_depth_bytes = dbytes * batch;
+    st_color_bytes = cbytes * batch;
     return TSDF_OK;
 }
 

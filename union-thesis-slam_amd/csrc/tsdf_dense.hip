@@ -298,10 +298,10 @@ static int dense_create(const int64_t dims[3], const int64_t index_offset[3], in
             h->b.vol.sb[0] = 0;
             h->b.vol.sb[1] = h->b.vol.sb[2] = 3;
         }
-        h->b.set_batch(xstride > kBrickEdge ? kMaxBatch : kFullBatch);
+        r = h->b.set_batch(xstride > kBrickEdge ? kMaxBatch : kFullBatch);
         const int64_t last = h->b.vol.nb[0] - 1;
         const int64_t gx_max = (int64_t)h->b.vol.off[0] + (last >> 1) * 2 * (int64_t)xstride + (last & 1) * (int64_t)xodd + kBrickEdge;
-        if (gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
+        if (r == TSDF_OK && gx_max > (1 << 24)) r = set_error(TSDF_E_ARG, "shard x extent out of range");
     }
     if (r == TSDF_OK) {
         // three-stage pipeline launches; TSDF_PIPELINE=0 forces the in-line path

@@ -116,13 +116,9 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #endif
 // Per-set list counters (reset by the prep of the batch): word c = entries of cost class c
 // (1..kMaxBatch); words kDoneWord / kDoneWordC = integrate and cull workgroups finished (fused hash
-// launch; the launch counts on its cull's set, or on its integrate's set when it has no cull);
-// words kQueueWord .. +7 = the fused integrate's per-XCD item queues (TSDF_GLOBAL_TAKE).
-constexpr int kDoneWord = kMaxBatch + 8, kDoneWordC = kMaxBatch + 9, kQueueWord = kMaxBatch + 16;
-constexpr int kCountWords = kQueueWord + 16;
-#ifndef TSDF_GLOBAL_TAKE  // fused launches: integrate items taken from per-XCD queues (integrate_items)
-#define TSDF_GLOBAL_TAKE 0
-#endif
+// launch; the launch counts on its cull's set, or on its integrate's set when it has no cull).
+constexpr int kDoneWord = kMaxBatch + 8, kDoneWordC = kMaxBatch + 9;
+constexpr int kCountWords = kMaxBatch + 16;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 // The whole table in HBM (512 KB, L2-resident) for waves with a weight past the LDS part (long
 // runs: weights pass 4079 after ~4300 frames of a room seen from inside); 65536 keeps every colour
@@ -1132,21 +1128,21 @@ __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned
 
 template <bool HASH>
 __device__ inline void append_kept(const Vol& v, ListEntry* list, unsigned int* count, unsigned long long* s_stat,
-                                   int* res, unsigned e, unsigned fmask, const Table* tab = nullptr,
+                                   int* res, unsigned e, unsigned fmask, int ncls, const Table* tab = nullptr,
                                    const Pool* pool = nullptr) {
+    // ncls: the batch's frames (cost classes 1..ncls; wave-uniform)
     const int lane = lane_id();
     const int cls = __popc(fmask);
     const unsigned long long any = __ballot(cls != 0);
     if (!any) return;
     unsigned n_cls = 0, rank = 0;
-#pragma unroll
-    for (int c = 1; c <= kMaxBatch; ++c) {
+    for (int c = 1; c <= ncls; ++c) {
         const unsigned long long m = __ballot(cls == c);
         if (lane == c) n_cls = (unsigned)__popcll(m);
         if (cls == c) rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
     }
     unsigned base = 0;  // lanes 1..8 reserve their class's slots at once
-    if (lane >= 1 && lane <= kMaxBatch && n_cls) base = atomicAdd(&count[lane], n_cls);
+    if (lane >= 1 && lane <= ncls && n_cls) base = atomicAdd(&count[lane], n_cls);
     if (lane == 0) atomicAdd(&s_stat[ST_VISITED], (unsigned long long)__popcll(any));
     base = __shfl(base, cls);
     const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
@@ -1221,7 +1217,7 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
         const int bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
         append_kept<HASH>(v, list, count, s_stat, res, (unsigned)(((long long)bx * v.nb[1] + by) * v.nb[2] + bz),
-                          s_mask[wave * 64 + lane], P2 ? &tab : nullptr, pool);
+                          s_mask[wave * 64 + lane], bt.n, P2 ? &tab : nullptr, pool);
     }
     __syncthreads();
     flush_stats(s_stat, stats);
@@ -1250,7 +1246,7 @@ __device__ inline void cull_owned(const Vol& v, const Batch& bt, const Table& ta
         if (have && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
     }
     __syncthreads();
-    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u, &tab, pool);
+    if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u, bt.n, &tab, pool);
     __syncthreads();
     flush_stats(s_stat, stats);
 }
@@ -1303,17 +1299,16 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq, unsigned* gq);
+                                       unsigned& nuniq);
 template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU = false>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr,
-                                      unsigned* gq = nullptr) {
+                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
     unsigned nupd = 0, nuniq = 0;  // the wave's voxel updates over all its items (ST_VOXELS, ST_UNIQUE; wave-uniform)
     integrate_items<HASH, DK, CK, OW1, NZ, CU>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
-                                           s_next, wg, n_wg, res, nupd, nuniq, gq);
+                                           s_next, wg, n_wg, res, nupd, nuniq);
     if (lane_id() == 0 && nupd) {
         atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
         atomicAdd(&s_stat[ST_UNIQUE], (unsigned long long)nuniq);
@@ -1325,7 +1320,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq, unsigned* gq) {
+                                       unsigned& nuniq) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
@@ -1337,10 +1332,11 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
     // first, so that the round-robin hands every wave a similar amount of work (the longest-job-
     // first order of list scheduling)
     const unsigned nbk = (unsigned)(v.nb[0] * v.nb[1] * v.nb[2]);
+    // (cost classes 1..bt.n: the batch's frames)
+    const int ncls = __builtin_amdgcn_readfirstlane(bt.n);
     int total = 0;
-#pragma unroll
-    for (int c = 0; c < kMaxBatch; ++c) total += (int)min(coh_load(&count[c + 1]), nbk);
-    int c = kMaxBatch - 1;
+    for (int c = 0; c < ncls; ++c) total += (int)min(coh_load(&count[c + 1]), nbk);
+    int c = ncls - 1;
     unsigned k0 = 0;  // list ordinal where class c starts (classes visited in descending order)
     // the length of class c only (one scalar live across the items; the next class's is read when
     // the walk reaches it -- at most kMaxBatch - 1 times per wave)
@@ -1362,29 +1358,15 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         constexpr bool kPrio = HASH ? TSDF_PRIO_HASH != 0 : TSDF_PRIO != 0;
 #if TSDF_XCD_DEAL
         // XCD-aware dealing: the launch's workgroups go to the 8 XCDs round-robin (workgroup w on
-        // XCD w % 8), so dealing brick k to workgroup k mod n_wg would hand each XCD every 8th
+        // XCD (w + r) % 8, the rotation r carried over from the dispatches before: measured from
+        // the workgroups' XCC_ID registers, profiles/r05_shards/), so dealing brick k to workgroup
+        // k mod n_wg would hand each XCD every 8th
         // brick of the list, spread over the whole image.  Renumbered, workgroup w deals as
         // (w % 8) * n_wg/8 + w / 8: each XCD takes runs of n_wg/8 consecutive bricks (neighbours
         // in the cull's order), whose gathers share its L2.
-        const int wg_hw = wg;
         if ((n_wg & 7) == 0) wg = (wg & 7) * (n_wg >> 3) + (wg >> 3);
 #endif
-        // gq (fused launches, TSDF_GLOBAL_TAKE): the same XCD runs, but taken dynamically by every
-        // wave of the XCD from its queue gq[x], so that the launch ends when the XCD's last item
-        // does rather than its slowest workgroup's share (a shard's launch: ~35 items per
-        // workgroup, and workgroups sharing a CU run unevenly).  The queue's atomics are
-        // workgroup-scope: performed in the XCD's L2, which every workgroup of the XCD shares
-        // (an agent-scope atomic goes past the L2 and costs microseconds) -- so a
-        // queue is only ever taken from by the workgroups of one XCD (workgroup w on XCD w % 8).
-        [[maybe_unused]] const bool split = (n_wg & 7) == 0;
-        if (!split) gq = nullptr;  // (the queues need whole XCD groups of workgroups)
-        [[maybe_unused]] const unsigned run = split ? (unsigned)(n_wg >> 3) : (unsigned)n_wg;
-#if TSDF_XCD_DEAL
-        [[maybe_unused]] int xq = split ? (wg_hw & 7) : 0;
-#else
-        [[maybe_unused]] int xq = split ? (wg & 7) : 0;
-#endif
-        const unsigned mine = gq ? 0u : total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
+        const unsigned mine = total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
         const bool use_prio = kPrio && mine >= (HASH ? TSDF_PRIO_MIN_HASH : TSDF_PRIO_MIN);  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
         if (use_prio) __builtin_amdgcn_s_setprio(3);
@@ -1392,21 +1374,6 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // entry, before it integrates the current one -- one item held in reserve per wave)
         const auto take = [&](ListEntry& e, int& zoff) -> bool {
             unsigned j = 0;
-            if (gq) {
-                if (lane_id() == 0) j = __hip_atomic_fetch_add(gq + xq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                j = __builtin_amdgcn_readfirstlane(j);
-                const unsigned i = j / parts;
-                const long long k = (long long)(i / run) * n_wg + (long long)xq * run + (i % run);
-                if (k >= (long long)total) return false;
-                while (c > 0 && (unsigned)k - k0 >= nc) {
-                    k0 += nc;
-                    --c;
-                    nc = min(coh_load(&count[c + 1]), nbk);
-                }
-                e = list[(size_t)c * nbk + ((unsigned)k - k0)];
-                zoff = (int)(j % parts) * NZ;
-                return true;
-            }
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
             if (use_prio) {
@@ -1732,8 +1699,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
         constexpr int wpg = kFusedWG / 64;
         integrate_list<false, DK, 0, OW1, NZ, CU>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
-                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi, nullptr,
-                                             TSDF_GLOBAL_TAKE ? sg.count_i + kQueueWord : nullptr);
+                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
@@ -1828,8 +1794,7 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         __syncthreads();
         constexpr int wpg = kFusedHashWG / 64;
         integrate_list<true, DK, 0, true, 4, CU>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
-                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i,
-                                            TSDF_GLOBAL_TAKE ? sg.count_i + kQueueWord : nullptr);
+                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {

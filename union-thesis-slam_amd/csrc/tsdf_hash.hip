@@ -1256,7 +1256,7 @@ int tsdf_hash_create(const int64_t dims[3], const float origin[3], double voxel_
     if (r == TSDF_OK) {
         h->b.vol.shard = shard;
         h->b.vol.n_shards = n_shards;
-        h->b.set_batch(n_shards > 1 ? kMaxBatch : kFullBatch);
+        r = h->b.set_batch(n_shards > 1 ? kMaxBatch : kFullBatch);
         if (max_blocks <= 0) max_blocks = std::min<long long>(h->b.n_bricks, 1 << 16);
         max_blocks = std::max<long long>(std::min<long long>(max_blocks, h->b.n_bricks), 64);
         h->map_size = capacity;

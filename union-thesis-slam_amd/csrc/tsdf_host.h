@@ -72,14 +72,7 @@ struct Base {
     // frames per launch (<= kMaxBatch, the kernels' Batch capacity): kMaxBatch for shards of a
     // multi-GPU volume, kFullBatch for whole volumes (set_batch; TSDF_BATCH overrides)
     int batch = kMaxBatch;
-    void set_batch(int want) {
-        if (const char* e = getenv("TSDF_BATCH")) want = atoi(e);
-        batch = want < 1 ? 1 : want > kMaxBatch ? kMaxBatch : want;
-        defer_frames = batch < 8 ? batch : 8;
-        if (const char* e = getenv("TSDF_DEFER_FRAMES")) defer_frames = atoi(e);
-        defer_frames = defer_frames < 1 ? 1 : defer_frames > batch ? batch : defer_frames;
-        if (const char* e = getenv("TSDF_DEFER_DMA_FRAMES")) dma_grain = atoi(e) < 1 ? 1 : atoi(e);
-    }
+    int set_batch(int want);  // (tsdf_common.hip: also allocates buffer set 0's list)
     // frames a deferred per-frame batch collects (TSDF_DEFER) before it runs: 8 -- the host's
     // frame copies of the next batch overlap the ingest and integrate of this one at a finer
     // grain than a whole launch's 16 frames (TSDF_DEFER_FRAMES overrides)
@@ -87,8 +80,8 @@ struct Base {
     // deferred frames whose DMA is issued together while the batch fills (TSDF_DEFER_DMA_FRAMES)
     int dma_grain = 2;
     // Per-batch buffers of the CURRENT buffer set (use_set).
-    float* pyr = nullptr;      // kMaxBatch per-frame max-depth pyramids
-    unsigned* rgbx = nullptr;  // kMaxBatch per-frame packed RGB8 images
+    float* pyr = nullptr;      // `batch` per-frame max-depth pyramids
+    unsigned* rgbx = nullptr;  // `batch` per-frame packed RGB8 images
     int pyr_H = 0, pyr_W = 0;
     // per-batch list of (brick | frame mask << 24) kept by the cull: kMaxBatch sub-lists of
     // n_bricks entries, one per cost class (frames kept); count[c] = entries of class c (1..8)
@@ -116,7 +109,7 @@ struct Base {
     void* st_depth[kSlots] = {};
     void* st_color[kSlots] = {};
     size_t st_depth_bytes = 0, st_color_bytes = 0;
-    unsigned short* dmask = nullptr;  // kMaxBatch masked u16 depth images (TSDF_DEPTH_INVALID_65535)
+    unsigned short* dmask = nullptr;  // `batch` masked u16 depth images (TSDF_DEPTH_INVALID_65535)
     size_t dmask_px = 0;
     void* hst_depth[kSlots] = {};      // page-locked bounce slots (hipHostMalloc)
     void* hst_color[kSlots] = {};
@@ -140,8 +133,8 @@ struct Base {
                    const double* K, const double* T, double ow);
     int stage_alloc(size_t dbytes, size_t cbytes);  // bounce + device staging slots (per frame)
     bool stage_fits(int dk, int ck, int H, int W) const {  // frames of this size need no reallocation
-        return st_depth_bytes >= frame_bytes_depth(dk, H, W) * kMaxBatch &&
-               st_color_bytes >= frame_bytes_color(ck, H, W) * kMaxBatch;
+        return st_depth_bytes >= frame_bytes_depth(dk, H, W) * batch &&
+               st_color_bytes >= frame_bytes_color(ck, H, W) * batch;
     }
 
     int init(int dev, const int64_t dims[3], const int64_t off[3], const float origin[3],
