@@ -52,7 +52,7 @@ def main():
               "hash": lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
                                                     max_blocks=1 << 15)}
     out = {"frames": nd, "passes": passes, "defer_frames": per}
-    # (a -DTSDF_DIAG build: the hash flush's host time by part, tsdf_diag_host_times)
+    # (a -DTSDF_HOST_TIMES build: the hash flush's host time by part, tsdf_diag_host_times)
     lib = _ffi.load()
     host_times = getattr(lib, "tsdf_diag_host_times", None) if hasattr(lib, "tsdf_diag_host_times") else None
     buf = (ctypes.c_double * 8)()

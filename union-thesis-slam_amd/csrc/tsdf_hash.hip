@@ -17,7 +17,7 @@
 
 #include "tsdf_host.h"
 
-#ifdef TSDF_DIAG
+#ifdef TSDF_HOST_TIMES
 // (diagnostic builds, tools/gpu/dropin_trace.py) host time of the hash drop-in's flush, by part:
 // 0 whole deferred flushes, 1 waiting for a pool report, 2 prepare_batch, 3 kernel launches,
 // 4 the call's end (k_free_unused), 5 flushes counted
@@ -1162,7 +1162,7 @@ int hash_settle(tsdf_hash* h) {
 // bricks re-run exactly before any later frame is integrated.
 int hash_flush(tsdf_hash* h, bool wait = true) {
     Base& B = h->b;
-#ifdef TSDF_DIAG
+#ifdef TSDF_HOST_TIMES
     if (!wait && B.dfr.n) g_host_us[5] += 1.0;
     HostTimer whole(wait || !B.dfr.n ? 7 : 0);
 #endif
@@ -1759,7 +1759,7 @@ extern "C" int tsdf_diag_wg_times_hash(unsigned long long* out) {
 }
 #endif
 
-#ifdef TSDF_DIAG
+#ifdef TSDF_HOST_TIMES
 // (diagnostic builds) the drop-in flush's host times (g_host_us above), read and cleared
 extern "C" int tsdf_diag_host_times(double* out) {
     for (int i = 0; i < 8; ++i) {
