@@ -8,7 +8,7 @@
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 A step is one launch's batch of frames (the unit the kernels fuse: one three-stage k_fused launch
-integrates 16 frames with the brick state held in registers; TSDFVolume.frames_per_launch).  The F synthetic frames
+integrates 32 frames with the brick state held in registers; TSDFVolume.frames_per_launch).  The F synthetic frames
 (tsdf_amd.scene: ray-cast room with spheres seen from the BENCH_RING trajectory, mean V_f 11.7 %
 of the volume; u16 millimetre depth, RGB) are generated directly in HBM before timing; W warmup
 steps, then K timed steps issued asynchronously, bracketed by barrier + synchronize; the max over
@@ -45,7 +45,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOM = 10.24
 VOXEL = 0.02
 PIX = 640 * 480
-BATCH = 16  # frames per step = frames per launch (set from the library: TSDFVolume.frames_per_launch)
+BATCH = 32  # frames per step = frames per launch (set from the library: TSDFVolume.frames_per_launch)
 WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) into 512^3 @ 2 cm dense grid"
 # the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), quoted only when
 # their workload AND the build id of the library they measured match the loaded library
@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one GPU each); default: the launcher's WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=250,
-                    help="timed steps (one launch's batch each: TSDFVolume.frames_per_launch() = 16 frames)")
+                    help="timed steps (one launch's batch each: TSDFVolume.frames_per_launch() = 32 frames)")
     ap.add_argument("--warmup", type=int, default=12, help="untimed steps")
     ap.add_argument("--frames", type=int, default=1000, help="synthetic frames resident in HBM")
     ap.add_argument("--no-hash", action="store_true")
@@ -396,14 +396,14 @@ def main():
     with contextlib.redirect_stdout(sys.stderr):  # the reference-style ctor prints; keep stdout JSON-only
         vol = grid_fusion.TSDFVolume(bnds, VOXEL, device=gpu, shard=(rank, n))
     global BATCH
-    BATCH = vol.frames_per_launch()  # a step = one launch's temporal batch (16 frames)
+    BATCH = vol.frames_per_launch()  # a step = one launch's temporal batch (32 frames)
     W, Ks = args.warmup, args.steps
     Wf, Kf = W * BATCH, Ks * BATCH
     cold = None
     if args.preheat_ms > 0:
         # Clock warm-up.  After the frame generation the GPU runs below its steady clock, and it
-        # takes it tens of milliseconds of load to get there: the driver's --steps 20 window (8 ms)
-        # measured cold reads ~13 % low (profiles/r04_clock/).  So the window is measured once
+        # takes it tens of milliseconds of load to get there: the driver's --steps 20 window (13 ms at
+        # round 4's 16-frame steps) measured cold read ~13 % low (profiles/r04_clock/).  So the window is measured once
         # cold (reported as cold_window), then the integrate runs untimed for preheat_ms, the
         # volume is reset, and the W warm-up and K timed steps run as always.
         run_timed(vol, depth, rgb, K, Tinv, 0, Wf, F, sync, barrier, False)

@@ -89,10 +89,11 @@ struct PyrGeo {
 // Up to kMaxBatch consecutive frames integrated by one launch (temporal batching: each voxel's
 // updates are still applied frame by frame, in order, so results are those of one-by-one
 // integration; the brick state is read and written once per batch instead of once per frame).
-// 16 frames per launch (round 4: +6 % dense and +19 % hash on one GPU, +7 % / +27 % on eighth
-// shards against 8, profiles/r04_e/); 8 remains a build option (-DTSDF_MAX_BATCH=8)
+// 32 frames per launch (round 5: +2.8 % dense and +8.4 % hash on one GPU on equal frames, +2 % /
+// +16 % on eighth shards against 16, profiles/r05_batch32/; round 4's 16 against 8: +6 % / +19 %,
+// profiles/r04_e/); 16 and 8 remain build options (-DTSDF_MAX_BATCH=16)
 #ifndef TSDF_MAX_BATCH
-#define TSDF_MAX_BATCH 16
+#define TSDF_MAX_BATCH 32
 #endif
 constexpr int kMaxBatch = TSDF_MAX_BATCH;
 static_assert(kMaxBatch == 8 || kMaxBatch == 16 || kMaxBatch == 32, "frames per batch: 8, 16 or 32");
