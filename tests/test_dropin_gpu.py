@@ -115,6 +115,9 @@ def test_async_hash_grows_ahead_of_the_pool(monkeypatch, pipe, vmm):
     from tsdf_amd import grid_fusion, hash_fusion
     monkeypatch.setenv("TSDF_PIPELINE", pipe)
     monkeypatch.setenv("TSDF_HASH_VMM", vmm)
+    # 8-frame launches: eight asynchronous launches after the synchronous start (with 32-frame
+    # launches the two left fit the room the start leaves, and nothing would need to grow)
+    monkeypatch.setenv("TSDF_BATCH", "8")
     d, c, poses = _synth(72, start=100)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     Tinv = np.linalg.inv(poses)

@@ -12,6 +12,7 @@
 #   prof               the round profile (tools/gpu/run_round_prof.sh)
 #   py:<script>[:args] python tools/gpu/<script> [args, '+'-separated]
 #   pylib:<lib>:<script>[:args]  the same with TSDF_HIP_LIB=abtest/lib<lib>.so
+#   tool:<script>[:args]:<tag>  python tools/<script> [args], output to <dir>/<tag>.out
 #   bin:<path>         a prebuilt probe binary (tools/gpu/<name>), output to <dir>/<name>.out
 #   kt:<script>[:args] the same under rocprofv3 --kernel-trace --stats (stats csv copied to <dir>)
 set -o pipefail
@@ -73,6 +74,10 @@ for step in "$@"; do
       IFS=: read -r _ l script args <<< "$step"
       TSDF_HIP_LIB=$(lib "$l") timeout -k 10 600 python -u "tools/gpu/$script" ${args//+/ } > "$O/${script%.py}_$l.out" \
         2> "$O/${script%.py}_$l.err" || exit 1
+      ;;
+    tool:*)
+      IFS=: read -r _ script args tag <<< "$step"
+      timeout -k 10 900 python -u "tools/$script" ${args//+/ } > "$O/$tag.out" 2> "$O/$tag.err" || exit 1
       ;;
     bin:*)
       b=${step#bin:}
