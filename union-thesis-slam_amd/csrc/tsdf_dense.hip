@@ -2,6 +2,7 @@
 // (grid_fusion.py:19-320).  HBM layout: three f32 SoA arrays of 512-voxel bricks, brick b =
 // (bx*nby + by)*nbz + bz, brick-local voxel (x*8 + y)*8 + z.
 #include <algorithm>
+#include <vector>
 #include <cstdlib>
 #include <cstring>
 
@@ -567,6 +568,8 @@ int tsdf_dense_set_profiling(tsdf_dense_t* h, int on) {
 extern "C" int tsdf_diag_wg_times(unsigned long long* out) {
     TSDF_HIP(hipDeviceSynchronize());
     TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 4 * kWgTimes));
+    static const std::vector<unsigned long long> zero(4 * (size_t)kWgTimes, 0ull);  // (read and cleared)
+    TSDF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wg_times), zero.data(), sizeof(unsigned long long) * 4 * kWgTimes));
     return TSDF_OK;
 }
 #endif

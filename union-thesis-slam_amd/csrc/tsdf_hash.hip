@@ -9,6 +9,7 @@
 // free list.  A voxel "entry" (count_num_hash_entries, get_hash_entry) is one bit of the
 // block's 512-bit occupancy mask, set by integrate or by an explicit insert.
 #include <algorithm>
+#include <vector>
 #include <climits>
 #include <chrono>
 #include <cstdlib>
@@ -1755,6 +1756,8 @@ int tsdf_hash_import_blocks(tsdf_hash_t* h, const int32_t* bxyz, int64_t n_block
 extern "C" int tsdf_diag_wg_times_hash(unsigned long long* out) {
     TSDF_HIP(hipDeviceSynchronize());
     TSDF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 4 * kWgTimes));
+    static const std::vector<unsigned long long> zero(4 * (size_t)kWgTimes, 0ull);  // (read and cleared)
+    TSDF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wg_times), zero.data(), sizeof(unsigned long long) * 4 * kWgTimes));
     return TSDF_OK;
 }
 #endif
