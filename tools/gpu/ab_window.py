@@ -53,7 +53,7 @@ def main():
         v.sync()
         dt = time.perf_counter() - t0
         st = v.stats()
-        return n / dt, 1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), st["voxel_updates"]
+        return n / dt, 1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), (st["voxel_updates"], st["bricks_visited"])
 
     out = {"lib": name, "build_id": _ffi.build_id()}
     bnds = np.array([[0.0, 10.24]] * 3)
@@ -78,8 +78,9 @@ def main():
     for _ in range(reps):
         vol.reset()
         run(vol, 0, 160, False, sync=False)
-        f, us, _ = run(vol, 160, 640, True, sync=False)
+        f, us, cnt = run(vol, 160, 640, True, sync=False)
         rows.append((f, us / B))
+    out["dense_fixed_updates_visited"] = cnt  # (the cull's kept bricks: a check of the pyramid)
     out["dense_fixed_fps"] = round(statistics.median(r[0] for r in rows), 1)
     out["dense_fixed_us_per_frame"] = round(statistics.median(r[1] for r in rows), 3)
     vol.close()

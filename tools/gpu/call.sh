@@ -4,7 +4,8 @@
 #   tests              pytest -m gpu (in-tree library) + smoke
 #   pytest:<args>      pytest -m gpu <args, '+'-separated> (a subset, e.g. pytest:tests/test_long_gpu.py+-k+config4)
 #   ab:<reps>:<a,b,..> driver-window A/B (tools/gpu/ab_window.py), libraries interleaved <reps>
-#                      times; "base" = in-tree, anything else = abtest/lib<name>.so
+#                      times; "base" = in-tree, VAR=VAL[+..] = in-tree with that environment,
+#                      anything else = abtest/lib<name>.so
 #   abs:<reps>:<a,b,..> tools/gpu/ab.sh: the bench and rank 0 of eighth dense / hash shards, per build
 #                      ("base", abtest/lib<name>.so, or VAR=VAL[+VAR2=VAL2] on the in-tree library)
 #   bench[:<args>]     bench.py --gpus 1 --steps 20 --warmup 5 [args, '+'-separated]
@@ -39,7 +40,12 @@ for step in "$@"; do
       IFS=, read -ra libs <<< "$names"
       for rep in $(seq 1 "$reps"); do
         for n in "${libs[@]}"; do
-          TSDF_HIP_LIB=$(lib "$n") timeout -k 10 300 python tools/gpu/ab_window.py 3 "$n" >> "$O/ab.jsonl" 2>> "$O/ab.err" || exit 1
+          if [[ $n == *=* ]]; then  # VAR=VAL[+VAR2=VAL2] on the in-tree library
+            IFS='+' read -ra envs <<< "$n"
+            env "${envs[@]}" timeout -k 10 300 python tools/gpu/ab_window.py 3 "$n" >> "$O/ab.jsonl" 2>> "$O/ab.err" || exit 1
+          else
+            TSDF_HIP_LIB=$(lib "$n") timeout -k 10 300 python tools/gpu/ab_window.py 3 "$n" >> "$O/ab.jsonl" 2>> "$O/ab.err" || exit 1
+          fi
         done
       done
       ;;

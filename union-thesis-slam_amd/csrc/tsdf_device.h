@@ -1531,26 +1531,44 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
                 make_uint4(a & 0xFFFFFFu, (a >> 24) | ((b & 0xFFFFu) << 8), (b >> 16) | ((cc & 0xFFu) << 16), cc >> 8);
         }
     }
+    const PyrGeo& pg = bt.pg;
+    const auto put = [&](int L, int X, int Y, float m) {
+        if (X < pg.w[L] && Y < pg.h[L]) pyr[pg.off[L] + Y * pg.w[L] + X] = m;
+    };
     if (act) {
         const int X = x0 >> 1, Y = y0 >> 1;
-        const PyrGeo& pg = bt.pg;
-        if (Y < pg.h[1]) {
-            if (X < pg.w[1]) pyr[pg.off[1] + Y * pg.w[1] + X] = ma;
-            if (X + 1 < pg.w[1]) pyr[pg.off[1] + Y * pg.w[1] + X + 1] = mb;
-        }
-        sa[r][2 * c] = ma;
-        sa[r][2 * c + 1] = mb;
+        put(1, X, Y, ma);
+        put(1, X + 1, Y, mb);
+    }
+    // levels 2 and 3 inside the wave (a wave holds 4 rows of 16 threads: the level-1 texels of
+    // 64 x 8 pixels): each level's 2x2 maximum from the lanes 1 / 16 / 32 apart (ds_bpermute, no
+    // barrier); only level 3 crosses waves, through LDS, and wave 0 reduces levels 4-6 the same way
+    // -- one workgroup barrier instead of five (the prep of a shard's batch is replicated on every
+    // rank: its workgroups are a fixed share of the launch's tail)
+    float m2 = fmaxf(ma, mb);
+    m2 = fmaxf(m2, __shfl_down(m2, 16));  // rows r, r + 1 (r even)
+    if (act && (r & 1) == 0) put(2, tx * 16 + c, ty * 16 + (r >> 1), m2);
+    float m3 = fmaxf(m2, __shfl_down(m2, 1));
+    m3 = fmaxf(m3, __shfl_down(m3, 32));  // level-2 rows r/2, r/2 + 1 (r % 4 == 0), columns c, c + 1
+    if (act && (r & 3) == 0 && (c & 1) == 0) {
+        put(3, tx * 8 + (c >> 1), ty * 8 + (r >> 2), m3);
+        sa[r >> 2][c >> 1] = m3;
     }
     __syncthreads();
-    pyr_level<0>(bt.pg, pyr, 2, sa, sb, 16, tx, ty);
-    __syncthreads();
-    pyr_level<0>(bt.pg, pyr, 3, sb, sa, 8, tx, ty);
-    __syncthreads();
-    pyr_level<0>(bt.pg, pyr, 4, sa, sb, 4, tx, ty);
-    __syncthreads();
-    pyr_level<0>(bt.pg, pyr, 5, sb, sa, 2, tx, ty);
-    __syncthreads();
-    pyr_level<0>(bt.pg, pyr, 6, sa, sb, 1, tx, ty);
+    if (t < 64) {  // wave 0: the tile's 8 x 8 level-3 texels, lane = y * 8 + x
+        const int lx = t & 7, ly = t >> 3;
+        float m = sa[ly][lx];
+        m = fmaxf(m, __shfl_down(m, 1));
+        m = fmaxf(m, __shfl_down(m, 8));
+        if ((lx & 1) == 0 && (ly & 1) == 0) put(4, tx * 4 + (lx >> 1), ty * 4 + (ly >> 1), m);
+        m = fmaxf(m, __shfl_down(m, 2));
+        m = fmaxf(m, __shfl_down(m, 16));
+        if ((lx & 3) == 0 && (ly & 3) == 0) put(5, tx * 2 + (lx >> 2), ty * 2 + (ly >> 2), m);
+        m = fmaxf(m, __shfl_down(m, 4));
+        m = fmaxf(m, __shfl_down(m, 32));
+        if (t == 0) put(6, tx, ty, m);
+    }
+    (void)sb;
 }
 
 template <int DK = 0>
