@@ -54,7 +54,7 @@ PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r05.json")
 SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r05.json")
 HASH_WORKLOAD = ("config[2]: the same frames into a voxel hash over the 512^3 @ 2 cm extent (8^3 blocks, 2^22 "
                  "slots, pool grown from 2^15 blocks)")
-HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r05.json")  # traffic + SQ of k_fused_hash<0>
+HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r05.json")  # traffic + SQ of k_fused_hash<0, true>
 
 
 def log(*a):
@@ -135,11 +135,16 @@ def attach_profiles(roof, st, build_id, pmc_path, sq_path, workload):
         if key == "traffic" and p.get("hbm_bytes_per_launch"):
             tb = float(p["hbm_bytes_per_launch"])
             roof["traffic"] = round(tb)
-            # measured DRAM-side bytes over this run's average launch time
+            # measured L2 memory-side bytes over this run's average launch time
             roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             roof["traffic_over_algorithmic"] = round(tb / roof["bytes_per_launch"], 3)
             roof["traffic_source"] = (rel + " (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH "
                                       "doubled per the gfx950 rule; build " + build_id + ")")
+            roof["traffic_note"] = ("FETCH/WRITE_SIZE count the L2's memory-side requests, Infinity-Cache (256 MB) "
+                                    "hits included: the excess over the algorithmic bytes is the frames' depth / "
+                                    "colour gathers refetched into the 4 MB per-XCD L2s by every brick projecting "
+                                    "onto them (a launch's 32 frames of images, ~60 MB, stay in the Infinity "
+                                    "Cache), not DRAM re-reads that a counter could separate (DESIGN.md §4)")
         med = p.get("median_per_launch", {})
         if key == "valu" and med.get("SQ_INSTS_VALU"):
             vox_launch = st["voxel_updates"] / st["kernel_launches"]
@@ -428,7 +433,7 @@ def main():
     vox = sum_over_ranks(float(st["voxel_updates"]))
     fps = Kf / dt_max
     kernel_s = st["kernel_ms"] / 1e3
-    roof = integrate_roofline(st, Kf, "tsdf::k_fused<true, 4, 0>: integrates batch k (and culls k+1, preps k+2 in "
+    roof = integrate_roofline(st, Kf, "tsdf::k_fused<true, 4, 0, true>: integrates batch k (and culls k+1, preps k+2 in "
                                       "the same launch)", first_timed)
     if roof is not None:
         attach_profiles(roof, st, _ffi.build_id(), PMC_PROFILE, SQ_PROFILE, WORKLOAD)
@@ -571,7 +576,7 @@ def main():
                                         "pool_capacity_in_run: before it, with the growth headroom of the "
                                         "launches in flight); dense: three f32 arrays of the volume",
                     "roofline": None}
-        hroof = integrate_roofline(hs, Kf, "tsdf::k_fused_hash<0>: integrates batch k (find-or-insert of its "
+        hroof = integrate_roofline(hs, Kf, "tsdf::k_fused_hash<0, true>: integrates batch k (find-or-insert of its "
                                            "blocks), culls k+1 and preps k+2 in the same launch; the window "
                                            "inserts blocks_allocated_in_window blocks",
                                    blocks_touched=hs["bricks_touched"])

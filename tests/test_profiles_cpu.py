@@ -116,7 +116,7 @@ def test_summaries_pick_the_timed_launches(tmp_path):
 
 def test_hash_profile_takes_the_inserting_window():
     """tools/summarize_profile.py hash: the bench's hash leg ends with the timed call (K + 2
-    launches of k_fused_hash<0>: two pipeline fills, then K integrating) and the no-allocation
+    launches of k_fused_hash<0, true>: two pipeline fills, then K integrating) and the no-allocation
     repeat (K + 2 more); the inserting window is the first call's K integrating launches."""
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tools"))
@@ -129,9 +129,9 @@ def test_hash_profile_takes_the_inserting_window():
             w = csv.DictWriter(f, ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
             w.writeheader()
             for i, v in enumerate(vals):
-                w.writerow({"Dispatch_Id": 10 + i, "Kernel_Name": "void tsdf::k_fused_hash<0>(...)",
+                w.writerow({"Dispatch_Id": 10 + i, "Kernel_Name": "void tsdf::k_fused_hash<0, true>(...)",
                             "Counter_Name": "FETCH_SIZE", "Counter_Value": v})
-                w.writerow({"Dispatch_Id": 10 + i, "Kernel_Name": "void tsdf::k_fused<true, 4, 0>(...)",
+                w.writerow({"Dispatch_Id": 10 + i, "Kernel_Name": "void tsdf::k_fused<true, 4, 0, true>(...)",
                             "Counter_Name": "FETCH_SIZE", "Counter_Value": -1.0})
         ins, rep = sp.hash_windows(p)
     assert [r["FETCH_SIZE"] for r in ins] == [100.0 + i for i in range(K)]

@@ -8,7 +8,7 @@
 #                      anything else = abtest/lib<name>.so
 #   abs:<reps>:<a,b,..> tools/gpu/ab.sh: the bench and rank 0 of eighth dense / hash shards, per build
 #                      ("base", abtest/lib<name>.so, or VAR=VAL[+VAR2=VAL2] on the in-tree library)
-#   bench[:<args>]     bench.py --gpus 1 --steps 20 --warmup 5 [args, '+'-separated]
+#   bench[@tag][:<args>]  bench.py --gpus 1 --steps 20 --warmup 5 [args, '+'-separated] -> bench[_tag].json
 #   sq[:<lib>]         one rocprofv3 --pmc SQ pass over the dense + hash bench legs
 #   prof               the round profile (tools/gpu/run_round_prof.sh)
 #   py:<script>[:args] python tools/gpu/<script> [args, '+'-separated]
@@ -55,8 +55,11 @@ for step in "$@"; do
       bash tools/gpu/ab.sh "$O/abs" "$reps" "${libs[@]}" > "$O/abs.out" 2>&1 || exit 1
       ;;
     bench*)
-      args=${step#bench}; args=${args#:}; args=${args//+/ }
-      timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 $args > "$O/bench.json" 2> "$O/bench.err" || exit 1
+      # bench[@tag][:args]: output <dir>/bench[_tag].json
+      head=${step%%:*}; tag=${head#bench}; tag=${tag#@}
+      args=""; [[ $step == *:* ]] && args=${step#*:}; args=${args//+/ }
+      out="$O/bench${tag:+_$tag}"
+      timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 $args > "$out.json" 2> "$out.err" || exit 1
       ;;
     sq*)
       l=${step#sq}; l=${l#:}

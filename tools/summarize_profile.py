@@ -9,11 +9,11 @@ bench line printed under the profiler):
   profiles/pmc_integrate_<tag>.json    HBM traffic per timed integrate launch (FETCH_SIZE/WRITE_SIZE)
   profiles/pmc_sq_<tag>.json           SQ issue counters per timed integrate launch
   profiles/pmc_hash_<tag>.json         the same counters (traffic + SQ) of the hash launch
-                                       k_fused_hash<0> in the bench's inserting hash window (and,
+                                       k_fused_hash<0, true> in the bench's inserting hash window (and,
                                        as a second block, in its no-allocation repeat window)
 
 The timed launches: every bench.py call of n batches issues n + 2 pipelined launches of
-k_fused<true, 4, 0> (the cold window, the clock warm-up, the W warm-up steps, then the timed call,
+k_fused<true, 4, 0, true> (the cold window, the clock warm-up, the W warm-up steps, then the timed call,
 whose first two launches fill the pipeline); the bench line records the dispatch-order index of
 the first timed integrate launch (roofline.first_timed_launch_index), and the K launches from it
 are the timed ones.
@@ -31,7 +31,7 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "tsdf::k_fused<true, 4, 0>"
+KERNEL = "tsdf::k_fused<true, 4, 0, true>"  # (CU = true: u32 colour registers, the canonical volume)
 W, K = 5, 20  # the driver's --warmup / --steps
 
 
@@ -153,13 +153,13 @@ def sq(tag):
     print(json.dumps(out, indent=1))
 
 
-HASH_KERNEL = "k_fused_hash<0>"
+HASH_KERNEL = "k_fused_hash<0, true>"
 SQ_NAMES = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
             "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
 
 
 def hash_windows(path):
-    """Per-dispatch counters of k_fused_hash<0> in one pass -> (inserting window, repeat window):
+    """Per-dispatch counters of k_fused_hash<0, true> in one pass -> (inserting window, repeat window):
     the hash leg ends with the timed call (K + 2 launches: two pipeline fills, then K integrating)
     and the no-allocation repeat (K + 2 more), the process's last 2 (K + 2) launches of the kernel."""
     per = {}
