@@ -3,6 +3,7 @@
 # Steps run in order, each under its own time limit; the call stops at the first failure.
 #   tests              pytest -m gpu (in-tree library) + smoke
 #   pytest:<args>      pytest -m gpu <args, '+'-separated> (a subset, e.g. pytest:tests/test_long_gpu.py+-k+config4)
+#   pytestlib:<lib>:<args>  the same with TSDF_HIP_LIB=abtest/lib<lib>.so
 #   ab:<reps>:<a,b,..> driver-window A/B (tools/gpu/ab_window.py), libraries interleaved <reps>
 #                      times; "base" = in-tree, VAR=VAL[+..] = in-tree with that environment,
 #                      anything else = abtest/lib<name>.so
@@ -34,6 +35,11 @@ for step in "$@"; do
       args=${step#pytest:}; args=${args//+/ }
       timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
         $args > "$O/pytest_subset.log" 2>&1 || { echo "pytest subset failed" >> "$O/steps.log"; exit 1; }
+      ;;
+    pytestlib:*)
+      IFS=: read -r _ l args <<< "$step"; args=${args//+/ }
+      TSDF_HIP_LIB=$(lib "$l") timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider $args > "$O/pytest_$l.log" 2>&1 || { echo "pytest $l failed" >> "$O/steps.log"; exit 1; }
       ;;
     ab:*)
       IFS=: read -r _ reps names <<< "$step"
