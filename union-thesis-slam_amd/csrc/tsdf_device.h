@@ -112,9 +112,6 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_SNAKE  // integrate_items: deal the list's rounds to workgroups in alternating directions
-#define TSDF_SNAKE 0
-#endif
 #ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU;
 #define TSDF_COLOR_U32 1  // round 5: dense -1.5 %, hash -1.5 % time per launch, profiles/r05_ab/)
 #endif
@@ -122,12 +119,7 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 // (1..kMaxBatch); words kDoneWord / kDoneWordC = integrate and cull workgroups finished (fused hash
 // launch; the launch counts on its cull's set, or on its integrate's set when it has no cull).
 constexpr int kDoneWord = kMaxBatch + 8, kDoneWordC = kMaxBatch + 9;
-// words kQueueWord .. +7: the fused integrate's tail queues (TSDF_DYN_TAIL, integrate_items)
-constexpr int kQueueWord = kMaxBatch + 16;
-constexpr int kCountWords = kQueueWord + 16;
-#ifndef TSDF_DYN_TAIL  // fused launches: the last TSDF_DYN_TAIL/16 of the list taken dynamically
-#define TSDF_DYN_TAIL 0
-#endif
+constexpr int kCountWords = kMaxBatch + 16;
 constexpr int kRcpTab = 4096;  // LDS table of RN(1/n), n < kRcpTab (32 KB per workgroup)
 // The whole table in HBM (512 KB, L2-resident) for waves with a weight past the LDS part (long
 // runs: weights pass 4079 after ~4300 frames of a room seen from inside); 65536 keeps every colour
@@ -446,8 +438,8 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 // depth_raw is unused and depth_m loads.
 // The per-step gathers go through structured buffer descriptors (stride = texel size, idxen):
 // the hardware scales the pixel index (p < 2^28, check_frame_args), so there is no shift or
-// 64-bit address arithmetic per gather.  num_records = pixels of the image; non-candidate steps
-// read pixel 0.
+// 64-bit address arithmetic per gather.  num_records = pixels of the image: a non-candidate step's
+// gather (discarded) reads the pixel its index names, or 0 past the image.
 __device__ unsigned short buf_ld_u16(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
                                      int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i16");
 __device__ unsigned buf_ld_u32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
@@ -655,7 +647,9 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
         // np.linalg.inv: all NaN -- fails z > 0)
         cand[k] = in[k] & ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
-        pix[k] = cand[k] ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
+        // (no select for the others: their gather is discarded, and an index past the image reads
+        // 0 from the buffer descriptor's bounds -- num_records = H * W, frame_bufs)
+        pix[k] = __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k];  // v_mad_u32_u24
     }
     // phase 2: gather depth and colour for every step at once, before the depth test, so
     // all the gathers share one memory latency (non-candidates read pixel 0, discarded).  The
@@ -1308,17 +1302,16 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq, unsigned* gq);
+                                       unsigned& nuniq);
 template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU = false>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr,
-                                      unsigned* gq = nullptr) {
+                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
     unsigned nupd = 0, nuniq = 0;  // the wave's voxel updates over all its items (ST_VOXELS, ST_UNIQUE; wave-uniform)
     integrate_items<HASH, DK, CK, OW1, NZ, CU>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
-                                           s_next, wg, n_wg, res, nupd, nuniq, gq);
+                                           s_next, wg, n_wg, res, nupd, nuniq);
     if (lane_id() == 0 && nupd) {
         atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
         atomicAdd(&s_stat[ST_UNIQUE], (unsigned long long)nuniq);
@@ -1330,7 +1323,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq, unsigned* gq) {
+                                       unsigned& nuniq) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
@@ -1376,51 +1369,13 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
         // in the cull's order), whose gathers share its L2.
         if ((n_wg & 7) == 0) wg = (wg & 7) * (n_wg >> 3) + (wg >> 3);
 #endif
-        // gq (fused launches, TSDF_DYN_TAIL): only the list's first S bricks are dealt; the rest --
-        // the cheapest, at the end of the longest-first order -- are taken dynamically from eight
-        // device-wide queues (agent-scope atomics: a few microseconds each, paid by tail items only)
-        // by whichever waves finish their share first, so that workgroups (and CUs) that drew
-        // dearer bricks do not set the launch's end alone
-        const int S = gq ? total - (int)(((long long)total * TSDF_DYN_TAIL) >> 4) : total;
-        [[maybe_unused]] const int dlen = (total - S + 7) >> 3;  // bricks per tail queue
-        [[maybe_unused]] int dq = wg & 7, dtried = 0;
-        [[maybe_unused]] bool dyn = false;
-        const unsigned mine = S > wg ? (unsigned)((S - wg + n_wg - 1) / n_wg) * parts : 0u;
+        const unsigned mine = total > wg ? (unsigned)((total - wg + n_wg - 1) / n_wg) * parts : 0u;
         const bool use_prio = kPrio && mine >= (HASH ? TSDF_PRIO_MIN_HASH : TSDF_PRIO_MIN);  // (wave-uniform)
         [[maybe_unused]] int prio = 3;
         if (use_prio) __builtin_amdgcn_s_setprio(3);
         // (TSDF_ITEM_PREFETCH: each wave takes its next item, and issues the load of its list
         // entry, before it integrates the current one -- one item held in reserve per wave)
-        const auto walk = [&](unsigned k) {
-            if (k < k0) {  // (a tail item below the walk's position: walk the classes from the top again)
-                c = ncls - 1;
-                k0 = 0;
-                nc = min(coh_load(&count[c + 1]), nbk);
-            }
-            while (c > 0 && k - k0 >= nc) {
-                k0 += nc;
-                --c;
-                nc = min(coh_load(&count[c + 1]), nbk);
-            }
-        };
-        const auto take_tail = [&](ListEntry& e, int& zoff) -> bool {
-            for (;;) {
-                unsigned j = 0;
-                if (lane_id() == 0) j = atomicAdd(gq + dq, 1u);
-                j = __builtin_amdgcn_readfirstlane(j);
-                const int b = S + dq * dlen + (int)(j / parts);
-                if (b < min(S + (dq + 1) * dlen, total)) {
-                    walk((unsigned)b);
-                    e = list[(size_t)c * nbk + ((unsigned)b - k0)];
-                    zoff = (int)(j % parts) * NZ;
-                    return true;
-                }
-                if (++dtried == 8) return false;
-                dq = (dq + 1) & 7;  // this queue is empty: the next one
-            }
-        };
         const auto take = [&](ListEntry& e, int& zoff) -> bool {
-            if (dyn) return take_tail(e, zoff);
             unsigned j = 0;
             if (lane_id() == 0) j = atomicAdd(s_next, 1u);
             j = __builtin_amdgcn_readfirstlane(j);
@@ -1437,21 +1392,13 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             // bricks dealt to workgroups (brick k to workgroup k mod n_wg), the parts of one brick
             // taken one after the other, so they run side by side on the workgroup's waves and
             // share their depth / colour gathers in the CU's cache
-#if TSDF_SNAKE
-            // rounds dealt in alternating directions (workgroup w takes w, then 2 n_wg - 1 - w, ...):
-            // along the longest-first list the first workgroups would otherwise draw the dearer
-            // brick of every round
-            const unsigned rnd = j / parts;
-            const long long k = (long long)rnd * n_wg + ((rnd & 1u) ? n_wg - 1 - wg : wg);
-#else
             const long long k = (long long)wg + (long long)(j / parts) * n_wg;  // increasing for this wave
-#endif
-            if (k >= (long long)S) {
-                if (S == total) return false;
-                dyn = true;  // the workgroup's share is taken: the tail queues
-                return take_tail(e, zoff);
+            if (k >= (long long)total) return false;
+            while (c > 0 && (unsigned)k - k0 >= nc) {
+                k0 += nc;
+                --c;
+                nc = min(coh_load(&count[c + 1]), nbk);
             }
-            walk((unsigned)k);
             e = list[(size_t)c * nbk + ((unsigned)k - k0)];
             zoff = (int)(j % parts) * NZ;
             return true;
@@ -1773,8 +1720,7 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
         constexpr int wpg = kFusedWG / 64;
         integrate_list<false, DK, 0, OW1, NZ, CU>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
-                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi, nullptr,
-                                             TSDF_DYN_TAIL ? sg.count_i + kQueueWord : nullptr);
+                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
@@ -1869,8 +1815,7 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
         __syncthreads();
         constexpr int wpg = kFusedHashWG / 64;
         integrate_list<true, DK, 0, true, 4, CU>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
-                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i,
-                                            TSDF_DYN_TAIL ? sg.count_i + kQueueWord : nullptr);
+                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
