@@ -112,12 +112,6 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_RCP32  // fused launches: an f32 copy of the LDS reciprocal table (integrate_brick)
-#define TSDF_RCP32 0
-#endif
-#ifndef TSDF_PZ_VGPR  // integrate_brick: the part's z coordinates in VGPRs (A/B)
-#define TSDF_PZ_VGPR 0
-#endif
 #ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU;
 #define TSDF_COLOR_U32 1  // round 5: dense -1.5 %, hash -1.5 % time per launch, profiles/r05_ab/)
 #endif
@@ -444,8 +438,8 @@ __device__ inline int table_find_or_insert(const Table& t, unsigned long long ke
 // depth_raw is unused and depth_m loads.
 // The per-step gathers go through structured buffer descriptors (stride = texel size, idxen):
 // the hardware scales the pixel index (p < 2^28, check_frame_args), so there is no shift or
-// 64-bit address arithmetic per gather.  num_records = pixels of the image: a non-candidate step's
-// gather (discarded) reads the pixel its index names, or 0 past the image.
+// 64-bit address arithmetic per gather.  num_records = pixels of the image; non-candidate steps
+// read pixel 0.
 __device__ unsigned short buf_ld_u16(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
                                      int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i16");
 __device__ unsigned buf_ld_u32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
@@ -653,9 +647,7 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
         // np.linalg.inv: all NaN -- fails z > 0)
         cand[k] = in[k] & ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
-        // (no select for the others: their gather is discarded, and an index past the image reads
-        // 0 from the buffer descriptor's bounds -- num_records = H * W, frame_bufs)
-        pix[k] = __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k];  // v_mad_u32_u24
+        pix[k] = cand[k] ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
     }
     // phase 2: gather depth and colour for every step at once, before the depth test, so
     // all the gathers share one memory latency (non-candidates read pixel 0, discarded).  The
@@ -706,12 +698,8 @@ template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU = false>
 __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool& pool,
                                        const Table& tab, ListEntry entry, int zoff,
                                        unsigned long long* s_stat, const double* s_rcp,
-                                       unsigned& nupd, unsigned& nuniq, int* res = nullptr,
-                                       const float* s_rcp32 = nullptr) {
+                                       unsigned& nupd, unsigned& nuniq, int* res = nullptr) {
     static_assert(!CU || (CK == 0 && OW1), "u32 colour registers: RGB8 frames, obs_weight 1");
-    // s_rcp32 (fused launches, TSDF_RCP32): f32(RN(1/n)) at the same byte offsets as s_rcp's f64
-    // entries -- the colour quotients' reciprocal without a conversion, and in free space (no tsdf
-    // quotient) without the f64 read
     // nupd: the wave's voxel updates, accumulated over its items (scalar popcounts of the step
     // masks; integrate_list adds it to the statistics once per wave); nuniq: the voxels among them
     // updated at least once in the batch (popcounts of the OR of each step's masks over the frames)
@@ -747,15 +735,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     constexpr int kPz = NZ < 8 ? NZ : 1;
     double pzs[kPz];
 #pragma unroll
-    for (int k = 0; k < kPz; ++k) {
-        pzs[k] = readlane_f64(pz_l, k + zoff);
-#if TSDF_PZ_VGPR
-        // held in VGPRs: fma(T10, pz, a2) then has one scalar operand (T10), where two scalar
-        // operands cost a v_mov per step and frame (one constant-bus read per VALU instruction);
-        // dense only (the hash kernel has no 8 VGPRs to spare)
-        if constexpr (!HASH) asm volatile("" : "+v"(pzs[k]));
-#endif
-    }
+    for (int k = 0; k < kPz; ++k) pzs[k] = readlane_f64(pz_l, k + zoff);
 
     // the brick's storage: dense brick b, or its hash pool block (wave-uniform; 32-bit for the hash,
     // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
@@ -930,35 +910,29 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const f2 w2 = {ws[k], ws[k + 1]};
                 const f2 a8 = pk_fma(w2, f2{8.0f, 8.0f}, f2{8.0f, 8.0f});  // byte offsets 8 * (w + 1)
                 const unsigned o0 = (unsigned)a8.x, o1 = (unsigned)a8.y;
-                const bool r32 = s_rcp32 && fast_t;  // (wave-uniform)
-                const auto load_y = [&](double (&y)[2]) {
-                    if (fast_t) {
-                        y[0] = *(const double*)((const char*)s_rcp + o0);
-                        y[1] = *(const double*)((const char*)s_rcp + o1);
-                    } else {
-                        y[0] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o0, 0, 0));
-                        y[1] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o1, 0, 0));
-                    }
-                };
                 double y[2];
+                if (fast_t) {
+                    y[0] = *(const double*)((const char*)s_rcp + o0);
+                    y[1] = *(const double*)((const char*)s_rcp + o1);
+                } else {
+                    y[0] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o0, 0, 0));
+                    y[1] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(rt, o1, 0, 0));
+                }
                 const f2 wn2 = w2 + 1.0f;
                 f2 r2;
-                if (r32) r2 = f2{*(const float*)((const char*)s_rcp32 + o0), *(const float*)((const char*)s_rcp32 + o1)};
                 if (free_space) {
-                    if (!r32) load_y(y);
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
                         tqv[k + j] = ts[k + j];
-                        if (!r32) r2[j] = (float)y[j];
+                        r2[j] = (float)y[j];
                     }
                 } else {
-                    load_y(y);
                     const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
                         const double num = (double)wt2[j] + dist_of(trunc, rtrunc, diff[k + j]);
                         tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
-                        if (!r32) r2[j] = (float)y[j];
+                        r2[j] = (float)y[j];
                     }
                 }
                 // colour (grid_fusion.py:302-314): float32, round half to even; decoded by bytes
@@ -1326,17 +1300,16 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq, const float* s_rcp32);
+                                       unsigned& nuniq);
 template <bool HASH, int DK, int CK, bool OW1, int NZ, bool CU = false>
 __device__ inline void integrate_list(const Vol& v, const Batch& bt, const Pool& pool, const Table& tab,
                                       const ListEntry* list, unsigned int* count, int n_list, int wave,
                                       int n_waves, unsigned long long* s_stat, const double* s_rcp,
-                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr,
-                                      const float* s_rcp32 = nullptr) {
+                                      unsigned* s_next = nullptr, int wg = 0, int n_wg = 1, int* res = nullptr) {
     wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the list walk stays scalar
     unsigned nupd = 0, nuniq = 0;  // the wave's voxel updates over all its items (ST_VOXELS, ST_UNIQUE; wave-uniform)
     integrate_items<HASH, DK, CK, OW1, NZ, CU>(v, bt, pool, tab, list, count, n_list, wave, n_waves, s_stat, s_rcp,
-                                           s_next, wg, n_wg, res, nupd, nuniq, s_rcp32);
+                                           s_next, wg, n_wg, res, nupd, nuniq);
     if (lane_id() == 0 && nupd) {
         atomicAdd(&s_stat[ST_VOXELS], (unsigned long long)nupd);
         atomicAdd(&s_stat[ST_UNIQUE], (unsigned long long)nuniq);
@@ -1348,7 +1321,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
                                        const ListEntry* list, unsigned int* count, int n_list, int wave,
                                        int n_waves, unsigned long long* s_stat, const double* s_rcp,
                                        unsigned* s_next, int wg, int n_wg, int* res, unsigned& nupd,
-                                       unsigned& nuniq, const float* s_rcp32) {
+                                       unsigned& nuniq) {
     constexpr int parts = 8 / NZ;  // waves per listed brick
     if (!count) {  // a flat list of n_list entries (hash overflow re-run)
         for (int e = wave; e < n_list * parts; e += n_waves)
@@ -1437,14 +1410,14 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             int zn = 0;
             const bool more = take(en, zn);
             // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res, s_rcp32);
+            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
             have = more;
             e = en;
             zoff = zn;
         }
 #else
         while (take(e, zoff))  // (the parts of a brick stay in one workgroup: the hash's z-halves meet in res)
-            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res, s_rcp32);
+            integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, e, zoff, s_stat, s_rcp, nupd, nuniq, res);
 #endif
         if (use_prio) __builtin_amdgcn_s_setprio(0);
         return;
@@ -1457,7 +1430,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             nc = min(coh_load(&count[c + 1]), nbk);
         }
         integrate_brick<HASH, DK, CK, OW1, NZ, CU>(item_vol(v), bt, pool, tab, list[(size_t)c * nbk + (k - k0)],
-                                               (e % parts) * NZ, s_stat, s_rcp, nupd, nuniq, res, s_rcp32);
+                                               (e % parts) * NZ, s_stat, s_rcp, nupd, nuniq, res);
     }
 }
 
@@ -1725,8 +1698,8 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     const Batch &bi = a.bi, &bc = a.bc, &bp = a.bp;
     unsigned long long* const stats = a.stats;
     const Stage& sg = a.sg;
-    // integrate: RN(1/n) table (+ its f32 copy, TSDF_RCP32); cull: per-brick frame masks; prep: pyramid tiles
-    __shared__ double s_buf[TSDF_RCP32 ? 2 * kRcpTab : kRcpTab];
+    // integrate: RN(1/n) table; cull: per-brick frame masks; prep: two pyramid tiles
+    __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ unsigned s_next;
     const int tid = threadIdx.x, b = blockIdx.x;
@@ -1739,19 +1712,13 @@ __global__ __launch_bounds__(kFusedWG) __attribute__((amdgpu_waves_per_eu(TSDF_D
     if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
         if (tid == 0) s_next = 0;
-        if (OW1) {
-            for (int i = tid; i < kRcpTab / 2; i += kFusedWG) {
-                const double2 r = ((const double2*)v.rcp)[i];
-                ((double2*)s_buf)[i] = r;
-                if (TSDF_RCP32) ((float4*)(s_buf + kRcpTab))[i] = make_float4((float)r.x, 0.0f, (float)r.y, 0.0f);
-            }
-        }
+        if (OW1)
+            for (int i = tid; i < kRcpTab / 2; i += kFusedWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedWG / 64;
         integrate_list<false, DK, 0, OW1, NZ, CU>(v, bi, pool, no_table, sg.list_i, sg.count_i, 0,
                                              b * wpg + (tid >> 6), sg.gi * wpg, s_stat,
-                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi, nullptr,
-                                             OW1 && TSDF_RCP32 ? (const float*)(s_buf + kRcpTab) : nullptr);
+                                             OW1 ? s_buf : nullptr, &s_next, b, sg.gi);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
@@ -1830,7 +1797,7 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
     const Batch &bi = a.bi, &bc = a.bc, &bp = a.bp;
     unsigned long long* const stats = a.stats;
     const Stage& sg = a.sg;
-    __shared__ double s_buf[TSDF_RCP32 ? 2 * kRcpTab : kRcpTab];
+    __shared__ double s_buf[kRcpTab];
     __shared__ unsigned long long s_stat[kNStat];
     __shared__ int s_last;
     __shared__ unsigned s_next;
@@ -1842,16 +1809,11 @@ __global__ __launch_bounds__(kFusedHashWG) __attribute__((amdgpu_waves_per_eu(TS
     if (b < sg.gi) {
         if (tid < kNStat) s_stat[tid] = 0;
         if (tid == 0) s_next = 0;
-        for (int i = tid; i < kRcpTab / 2; i += kFusedHashWG) {
-            const double2 r = ((const double2*)v.rcp)[i];
-            ((double2*)s_buf)[i] = r;
-            if (TSDF_RCP32) ((float4*)(s_buf + kRcpTab))[i] = make_float4((float)r.x, 0.0f, (float)r.y, 0.0f);
-        }
+        for (int i = tid; i < kRcpTab / 2; i += kFusedHashWG) ((double2*)s_buf)[i] = ((const double2*)v.rcp)[i];
         __syncthreads();
         constexpr int wpg = kFusedHashWG / 64;
         integrate_list<true, DK, 0, true, 4, CU>(v, bi, pool, tab, sg.list_i, sg.count_i, 0, b * wpg + (tid >> 6),
-                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i,
-                                            TSDF_RCP32 ? (const float*)(s_buf + kRcpTab) : nullptr);
+                                            sg.gi * wpg, s_stat, s_buf, &s_next, b, sg.gi, sg.res_i);
         __syncthreads();
         flush_stats(s_stat, stats);
     } else if (b < sg.gi + sg.gc) {
