@@ -112,9 +112,6 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_BCACHE  // the fused hash cull keeps each brick's block from batch to batch (Table::bcache)
-#define TSDF_BCACHE 0
-#endif
 #ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU;
 #define TSDF_COLOR_U32 1  // round 5: dense -1.5 %, hash -1.5 % time per launch, profiles/r05_ab/)
 #endif
@@ -192,9 +189,6 @@ struct Table {
     const int* owned;           // bucket-range shards: the bricks this shard owns, increasing (else null)
     int n_owned;
     int* ins_list;              // fused launches: bricks their culls inserted (k_free_unused; ins_cap)
-    int* bcache;                // fused culls: each brick's block as last found / inserted, -1 unknown
-                                // (n_bricks; TSDF_BCACHE; cleared by the host whenever blocks are freed
-                                // other than by k_free_unused, which clears its own bricks)
     long long ins_cap;
     int overflow_cap;
     int int_bits;               // 64: NumPy int64; 32: wrapping int32 (author's Windows run)
@@ -1086,17 +1080,6 @@ constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 
 __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned e, unsigned long long* s_stat,
                                           bool& fresh) {
     fresh = false;
-#if TSDF_BCACHE
-    // the brick's block from an earlier batch: block ids never change while the block lives, and a
-    // block is freed only with its cache entry (k_free_unused) or with the whole cache (host)
-    if (t.bcache) {
-        const int cb = t.bcache[e];
-        if (cb >= 0) {
-            atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
-            return cb;
-        }
-    }
-#endif
     const int nb12 = v.nb[1] * v.nb[2];
     const int bx = (int)e / nb12, r = (int)e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
     const unsigned long long key = pack_key(bx, by, bz);
@@ -1115,9 +1098,6 @@ __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned
             atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
             atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
             atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
-#if TSDF_BCACHE
-            if (t.bcache && b >= 0 && b < max_blocks) t.bcache[e] = b;
-#endif
             return (b >= 0 && b < max_blocks) ? b : kResFail;  // (a found key's value is always set)
         }
         if (k == kTomb) {
@@ -1129,9 +1109,6 @@ __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned
             if (blk < 0) return kResFail;  // pool exhausted
             if (atomicCAS(&keys[target], expect, key) == expect) {
                 coh_store(&vals[target], blk);
-#if TSDF_BCACHE
-                if (t.bcache) t.bcache[e] = blk;
-#endif
                 const unsigned long long i = atomicAdd((unsigned long long*)&t.st->n_inserted, 1ull);
                 if ((long long)i < t.ins_cap) t.ins_list[i] = (int)e;
                 atomicAdd(&s_stat[ST_ALLOC], 1ull);

@@ -436,7 +436,6 @@ __global__ void k_free_unused(Vol v, Table t) {
         bool used = false;
         for (int k = 0; k < 8; ++k) used |= coh_load(&t.occ[(size_t)blk * 8 + k]) != 0ull;
         if (used) continue;
-        if (t.bcache) t.bcache[e] = -1;  // (the brick's cache entry goes with its block)
         const long long nx = s + 1 == t.capacity ? 0 : s + 1;
         const bool last = coh_load(&t.keys[nx]) == kEmpty;
         coh_store(&t.vals[s], -1);  // (the empty-slot invariant, k_fill_keys)
@@ -962,10 +961,6 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         TSDF_HIP(hipMalloc(&h->d_ins, sizeof(int) * (size_t)B.n_bricks));
         h->t.ins_list = h->d_ins;
         h->t.ins_cap = B.n_bricks;
-        if (TSDF_BCACHE) {
-            TSDF_HIP(hipMalloc(&h->t.bcache, sizeof(int) * (size_t)B.n_bricks));
-            TSDF_HIP(hipMemsetAsync(h->t.bcache, 0xFF, sizeof(int) * (size_t)B.n_bricks, B.stream));
-        }
     }
     const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
     // (a shard that owns no brick -- more shards than bricks -- still runs one cull workgroup, which
@@ -1351,8 +1346,7 @@ int tsdf_hash_destroy(tsdf_hash_t* h) {
     if (!h) return TSDF_OK;
     (void)hipSetDevice(h->b.device);
     h->b.release();
-    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res, h->d_ins, h->t.bcache,
-                  (void*)h->t.owned};
+    void* ps[] = {h->t.keys, h->t.vals, h->t.overflow, h->t.st, h->d_list, h->d_res, h->d_ins, (void*)h->t.owned};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (h->vmm) {
@@ -1377,7 +1371,6 @@ int tsdf_hash_reset(tsdf_hash_t* h) {
     hipLaunchKernelGGL(k_fill_keys, dim3(2048), dim3(256), 0, B.stream, h->t.keys, h->t.vals,
                        (long long)h->t.capacity);
     TSDF_HIP(hipGetLastError());
-    if (h->t.bcache) TSDF_HIP(hipMemsetAsync(h->t.bcache, 0xFF, sizeof(int) * (size_t)B.n_bricks, B.stream));
     TSDF_HIP(hipMemsetAsync(h->t.st, 0, sizeof(PoolState), B.stream));
     TSDF_HIP(hipMemsetAsync(B.stats, 0, sizeof(unsigned long long) * kNStat * kStatSpread, B.stream));
     TSDF_HIP(hipStreamSynchronize(B.stream));
@@ -1529,8 +1522,6 @@ int tsdf_hash_remove(tsdf_hash_t* h, const int64_t* ijk, int64_t n, uint8_t* rem
         hipLaunchKernelGGL(k_free_empty, dim3((unsigned)((keys.size() + 255) / 256)), dim3(256), 0, B.stream,
                            h->t, (const unsigned long long*)dkeys, (long long)keys.size());
         TSDF_HIP(hipGetLastError());
-        // (blocks freed here may be handed to other bricks: the culls' brick -> block cache goes)
-        if (h->t.bcache) TSDF_HIP(hipMemsetAsync(h->t.bcache, 0xFF, sizeof(int) * (size_t)B.n_bricks, B.stream));
     }
     if (removed) TSDF_HIP(hipMemcpyAsync(removed, drem, n, hipMemcpyDeviceToHost, B.stream));
     TSDF_HIP(hipStreamSynchronize(B.stream));
