@@ -568,7 +568,9 @@ def main():
                                         "kernel_avg_us": round(1e3 * hs2["kernel_ms"] / max(1, hs2["kernel_launches"]), 2),
                                         "blocks_allocated": int(hs2["blocks_allocated"]),
                                         "note": "the same timed window integrated again into the table it left "
-                                                "(its blocks exist: no allocation); not the headline"},
+                                                "(every updated block exists; the culls still insert, and the call's end "
+                                                "frees, the few kept bricks no frame updates: blocks_allocated); not the "
+                                                "headline"},
                     "hbm_state_bytes": int(sum_over_ranks(hash_bytes)),
                     "dense_hbm_state_bytes": int(sum_over_ranks(dense_bytes)),
                     "state_bytes_note": "hash: table keys + slot->block map + block pool (tsdf/weight/"
