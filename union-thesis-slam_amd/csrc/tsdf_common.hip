@@ -134,7 +134,6 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
     device = dev;
     TSDF_HIP(hipSetDevice(device));
     if (const char* e = getenv("TSDF_CULL_G")) cull_g = atoi(e);  // A/B override (Base::cull_per_wg)
-    if (const char* e = getenv("TSDF_FUSED_GI_MULT")) gi_mult = std::max(1, std::min(16, atoi(e)));  // A/B
     for (int a = 0; a < 3; ++a) {
         const int64_t o = off ? off[a] : 0;
         if (dims[a] <= 0 || o < 0 || dims[a] + o > (1 << 24))

@@ -120,7 +120,7 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
     const int nb = (n_frames + nbat - 1) / nbat;
     const int gi_occ = h->nz == 4 ? (int)B.grid_for((const void*)k_fused<true, 4>, kFusedWG)
                                   : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
-    const int gi_full = (h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ) * B.gi_mult;
+    const int gi_full = h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ;
     const int gc_full = (int)B.cull_grid_fused();
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {

@@ -962,7 +962,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         h->t.ins_list = h->d_ins;
         h->t.ins_cap = B.n_bricks;
     }
-    const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG) * B.gi_mult;
+    const int gi_full = (int)B.grid_for((const void*)k_fused_hash<0>, kFusedHashWG);
     // (a shard that owns no brick -- more shards than bricks -- still runs one cull workgroup, which
     // lists nothing, like the in-line path's max(1, ...))
     const int gc_full = h->t.owned ? std::max(1, (h->t.n_owned + 63) / 64) : (int)B.cull_grid_fused();

@@ -179,9 +179,6 @@ struct Base {
     // ranks), 1 on smaller shards (the cull IS the launch's tail there: 3 cost 4.6 % on an eighth
     // shard); TSDF_CULL_G overrides.  And the cull workgroups of such a launch.
     int cull_g = 0;  // (0: by the rule)
-    // integrate workgroups of a fused launch per resident slot (TSDF_FUSED_GI_MULT, A/B): more than
-    // one lets the hardware dispatcher hand the next workgroup to whichever CU finishes first
-    int gi_mult = 1;
     int cull_per_wg() const {
         if (cull_g > 0) return cull_g < kCullGMax ? cull_g : kCullGMax;
         return cull_grid() >= 1024 ? 3 : 1;
