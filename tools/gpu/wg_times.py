@@ -92,6 +92,11 @@ def main():
         out["integrate"]["cus_by_wgs"] = {str(k): int((cnt == k).sum()) for k in np.unique(cnt)}
         out["integrate"]["busy_by_wgs_per_cu"] = {str(k): round(float(busy[per == k].mean()), 1) for k in np.unique(per)}
         cu_end = np.array([end_i[inv == j].max() for j in range(len(ucu))])
+        xcd_of_cu = (ucu >> np.uint64(8)).astype(np.int64)
+        out["integrate"]["cu_end_mean_by_xcd"] = {str(x): round(float(cu_end[xcd_of_cu == x].mean()), 1)
+                                                  for x in np.unique(xcd_of_cu)}
+        out["integrate"]["cu_end_max_by_xcd"] = {str(x): round(float(cu_end[xcd_of_cu == x].max()), 1)
+                                                 for x in np.unique(xcd_of_cu)}
         out["xcc_is_wg_mod_8"] = round(float(np.mean([r["xcc_rr"] for r in rows])), 4)
         out["integrate"]["cu_end_deciles"] = [round(float(x), 1) for x in np.percentile(cu_end, range(0, 101, 10))]
         print(json.dumps(out), flush=True)
