@@ -112,9 +112,6 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_ROT_DEAL  // integrate_items: rotate the deal's slice order from round to round (A/B)
-#define TSDF_ROT_DEAL 0
-#endif
 #ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU;
 #define TSDF_COLOR_U32 1  // round 5: dense -1.5 %, hash -1.5 % time per launch, profiles/r05_ab/)
 #endif
@@ -1393,21 +1390,7 @@ __device__ inline void integrate_items(const Vol& v, const Batch& bt, const Pool
             // bricks dealt to workgroups (brick k to workgroup k mod n_wg), the parts of one brick
             // taken one after the other, so they run side by side on the workgroup's waves and
             // share their depth / colour gathers in the CU's cache
-#if TSDF_ROT_DEAL
-            // the round's slice order rotated from round to round (XCD slice (x + 3r) % 8, offset
-            // (o + 29r) % slice): along the longest-first list each round's first slices hold its
-            // dearer bricks, and a fixed order hands them to the same XCD and workgroups every round
-            const unsigned rnd = j / parts;
-            long long k;
-            if ((n_wg & 7) == 0) {
-                const int per = n_wg >> 3, x = wg / per, o = wg - x * per;
-                k = (long long)rnd * n_wg + (long long)((x + 3 * (int)rnd) & 7) * per + (o + 29 * (long long)rnd) % per;
-            } else {
-                k = (long long)rnd * n_wg + (wg + 29 * (long long)rnd) % n_wg;
-            }
-#else
             const long long k = (long long)wg + (long long)(j / parts) * n_wg;  // increasing for this wave
-#endif
             if (k >= (long long)total) return false;
             while (c > 0 && (unsigned)k - k0 >= nc) {
                 k0 += nc;
