@@ -112,9 +112,6 @@ constexpr int kFullBatch = TSDF_FULL_BATCH < kMaxBatch ? TSDF_FULL_BATCH : kMaxB
 #ifndef TSDF_ITEM_PREFETCH  // take the next item before integrating the current one
 #define TSDF_ITEM_PREFETCH 0
 #endif
-#ifndef TSDF_CULL2  // the culls test one brick against two frames at a time (cull_pre / cull_post2)
-#define TSDF_CULL2 0
-#endif
 #ifndef TSDF_COLOR_U32  // fused launches on canonical volumes: colours held as u32 (integrate_brick CU;
 #define TSDF_COLOR_U32 1  // round 5: dense -1.5 %, hash -1.5 % time per launch, profiles/r05_ab/)
 #endif
@@ -344,91 +341,6 @@ __device__ inline bool cull_brick(const Vol& v, const Frame& fr, const PyrGeo& p
             if (ty0 + dy <= ty1 && tx0 + dx <= tx1) dmax = fmaxf(dmax, lvl[(ty0 + dy) * wl + tx0 + dx]);
     return dmax > 0.0f && dmax >= need;
 }
-
-#if TSDF_CULL2
-// cull_brick in two halves, so that a wave can test one brick against two frames with their memory
-// latencies overlapped (TSDF_CULL2): cull_pre does the frustum and projection work and yields the
-// pyramid window (the same tests and values as cull_brick); cull_post2 issues both windows' loads
-// before either maximum.
-struct CullPre {
-    bool live;      // survived the half-space, z and bbox tests
-    bool keep_all;  // window wider than 4x4 texels at the coarsest level: kept without a depth test
-    float need;
-    const float* lvl;
-    int wl, tx0, tx1, ty0, ty1;
-};
-__device__ inline CullPre cull_pre(const Vol& v, const Frame& fr, const PyrGeo& pg, const BrickBox& bb) {
-    CullPre c{};
-    bool live = true;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const float* q = fr.planes[i];
-        live = live & !(q[0] * bb.ctr[0] + q[1] * bb.ctr[1] + q[2] * bb.ctr[2] + q[3] < -bb.rad);
-    }
-    const double* T = fr.T;
-    float c0[3], d[3][3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        c0[r] = (float)(T[4 * r + 0] * bb.p0[0] + T[4 * r + 1] * bb.p0[1] + T[4 * r + 2] * bb.p0[2] + T[4 * r + 3]);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) d[r][a] = (float)T[4 * r + a] * bb.ext[a];
-    }
-    const float fx = (float)fr.fx, fy = (float)fr.fy, cx = (float)fr.cx, cy = (float)fr.cy;
-    float zmin = 3e38f, zmax = -3e38f, umin = 3e38f, umax = -3e38f, vmin = 3e38f, vmax = -3e38f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        float q[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-            q[r] = c0[r] + ((k & 1) ? d[r][0] : 0.0f) + ((k & 2) ? d[r][1] : 0.0f) + ((k & 4) ? d[r][2] : 0.0f);
-        zmin = fminf(zmin, q[2]);
-        zmax = fmaxf(zmax, q[2]);
-        const float iz = __builtin_amdgcn_rcpf(fmaxf(q[2], 1e-6f));
-        const float u = fx * q[0] * iz + cx, w = fy * q[1] * iz + cy;
-        umin = fminf(umin, u); umax = fmaxf(umax, u);
-        vmin = fminf(vmin, w); vmax = fmaxf(vmax, w);
-    }
-    live = live & !(zmax < -1e-4f);
-    int u0 = 0, u1 = fr.W - 1, v0 = 0, v1 = fr.H - 1;
-    if (zmin > 0.2f) {
-        const float fu0 = floorf(umin) - 1.0f, fu1 = ceilf(umax) + 1.0f;
-        const float fv0 = floorf(vmin) - 1.0f, fv1 = ceilf(vmax) + 1.0f;
-        live = live & !(fu1 < 0.0f || fv1 < 0.0f || fu0 > (float)(fr.W - 1) || fv0 > (float)(fr.H - 1));
-        u0 = (int)fmaxf(fu0, 0.0f); u1 = (int)fminf(fu1, (float)(fr.W - 1));
-        v0 = (int)fmaxf(fv0, 0.0f); v1 = (int)fminf(fv1, (float)(fr.H - 1));
-    }
-    int L = 1;
-    while (L < kPyrLevels && (((u1 >> L) - (u0 >> L)) > 3 || ((v1 >> L) - (v0 >> L)) > 3)) ++L;
-    c.need = zmin - (float)v.trunc - 1e-3f;
-    c.tx0 = u0 >> L; c.tx1 = u1 >> L; c.ty0 = v0 >> L; c.ty1 = v1 >> L;
-    c.keep_all = c.tx1 - c.tx0 > 3 || c.ty1 - c.ty0 > 3;
-    c.lvl = fr.pyr + pg.off[L];
-    c.wl = pg.w[L];
-    c.live = live;
-    return c;
-}
-__device__ inline void cull_post2(const CullPre& a, const CullPre& b, bool& ka, bool& kb) {
-    const bool la = a.live && !a.keep_all, lb = b.live && !b.keep_all;
-    float ta[16], tb[16];
-#pragma unroll
-    for (int dy = 0; dy < 4; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 4; ++dx) {
-            const bool pa = la && a.ty0 + dy <= a.ty1 && a.tx0 + dx <= a.tx1;
-            const bool pb = lb && b.ty0 + dy <= b.ty1 && b.tx0 + dx <= b.tx1;
-            ta[dy * 4 + dx] = pa ? a.lvl[(a.ty0 + dy) * a.wl + a.tx0 + dx] : 0.0f;
-            tb[dy * 4 + dx] = pb ? b.lvl[(b.ty0 + dy) * b.wl + b.tx0 + dx] : 0.0f;
-        }
-    float ma = 0.0f, mb = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        ma = fmaxf(ma, ta[i]);
-        mb = fmaxf(mb, tb[i]);
-    }
-    ka = a.live && (a.keep_all || (ma > 0.0f && ma >= a.need));
-    kb = b.live && (b.keep_all || (mb > 0.0f && mb >= b.need));
-}
-#endif
 
 // Take one block from the pool: the free list first, then the bump region.  `cursor` counts
 // this launch's allocations; k_commit folds it into free_count / pool_top afterwards, so both
@@ -1286,39 +1198,6 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
     const int n_sb = nsx * nsy * nsz;
     const int ex = 1 << v.sb[0], ey = 1 << v.sb[1], ez = 1 << v.sb[2];
     const int lz = lane & (ez - 1), ly = (lane >> v.sb[2]) & (ey - 1), lx = lane >> (v.sb[1] + v.sb[2]);
-#if TSDF_CULL2
-    // (superbrick g, frame f) pairs two at a time: pairs p and p + n_waves, tested together
-    for (int p = wave; p < G * bt.n; p += 2 * n_waves) {
-        const int p2 = p + n_waves;
-        const int g1 = p / bt.n, f1 = p - g1 * bt.n;
-        const bool two = p2 < G * bt.n;
-        const int g2 = two ? p2 / bt.n : g1, f2 = two ? p2 - g2 * bt.n : f1;
-        const int si1 = wgi * G + g1, si2 = wgi * G + g2;
-        const auto coords = [&](int si, int& bx, int& by, int& bz) {
-            const int sx = si / (nsy * nsz), sr = si - sx * (nsy * nsz), sy = sr / nsz, sz = sr - sy * nsz;
-            bx = sx * ex + lx, by = sy * ey + ly, bz = sz * ez + lz;
-        };
-        int ax, ay, az, bx2, by2, bz2;
-        coords(si1, ax, ay, az);
-        coords(si2, bx2, by2, bz2);
-        const bool ta = si1 < n_sb && ax < v.nb[0] && ay < v.nb[1] && az < v.nb[2];
-        const bool tb = two && si2 < n_sb && bx2 < v.nb[0] && by2 < v.nb[1] && bz2 < v.nb[2];
-        const Frame& fa = bt.f[f1];
-        const Frame& fb = bt.f[f2];
-        CullPre ca = cull_pre(v, fa, bt.pg, brick_box(v, fa.eye, ax, ay, az));
-        CullPre cb = cull_pre(v, fb, bt.pg, brick_box(v, fb.eye, bx2, by2, bz2));
-        ca.live = ca.live && ta;
-        cb.live = cb.live && tb;
-        if (HASH && v.n_shards > 1) {  // bucket-range ownership (shards use cull_owned)
-            ca.live = ca.live && shard_of<P2>(ref_hash<P2>(ax, ay, az, tab.shard_cap, tab.int_bits), v.n_shards, tab.shard_cap) == v.shard;
-            cb.live = cb.live && shard_of<P2>(ref_hash<P2>(bx2, by2, bz2, tab.shard_cap, tab.int_bits), v.n_shards, tab.shard_cap) == v.shard;
-        }
-        bool ka, kb;
-        cull_post2(ca, cb, ka, kb);
-        if (ka) atomicOr(&s_mask[g1 * 64 + lane], 1u << f1);
-        if (kb) atomicOr(&s_mask[g2 * 64 + lane], 1u << f2);
-    }
-#else
     for (int p = wave; p < G * bt.n; p += n_waves) {  // (superbrick g, frame f) pairs
         const int g = p / bt.n, f = p - g * bt.n;
         const int si = wgi * G + g;
@@ -1333,7 +1212,6 @@ __device__ inline void cull_superbrick(const Vol& v, const Batch& bt, const Tabl
         }
         if (test && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[g * 64 + lane], 1u << f);
     }
-#endif
     __syncthreads();
     const int si = wgi * G + wave;
     if (wave < G && si < n_sb) {  // append the kept bricks to the sub-list of their cost class (frames kept)
@@ -1364,27 +1242,10 @@ __device__ inline void cull_owned(const Vol& v, const Batch& bt, const Table& ta
     const int e = have ? tab.owned[i] : 0;
     const int nb12 = v.nb[1] * v.nb[2];
     const int bx = e / nb12, r = e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
-#if TSDF_CULL2
-    for (int f = wave; f < bt.n; f += 2 * n_waves) {  // two frames at a time (cull_post2)
-        const int f2 = f + n_waves;
-        const bool two = f2 < bt.n;
-        const Frame& fa = bt.f[f];
-        const Frame& fb = bt.f[two ? f2 : f];
-        CullPre ca = cull_pre(v, fa, bt.pg, brick_box(v, fa.eye, bx, by, bz));
-        CullPre cb = cull_pre(v, fb, bt.pg, brick_box(v, fb.eye, bx, by, bz));
-        ca.live = ca.live && have;
-        cb.live = cb.live && have && two;
-        bool ka, kb;
-        cull_post2(ca, cb, ka, kb);
-        if (ka) atomicOr(&s_mask[lane], 1u << f);
-        if (kb) atomicOr(&s_mask[lane], 1u << f2);
-    }
-#else
     for (int f = wave; f < bt.n; f += n_waves) {
         const Frame& fr = bt.f[f];
         if (have && cull_brick(v, fr, bt.pg, brick_box(v, fr.eye, bx, by, bz))) atomicOr(&s_mask[lane], 1u << f);
     }
-#endif
     __syncthreads();
     if (wave == 0) append_kept<HASH>(v, list, count, s_stat, res, (unsigned)e, have ? s_mask[lane] : 0u, bt.n, &tab, pool);
     __syncthreads();
