@@ -265,15 +265,16 @@ def test_cyclic_column_shards_reassemble_bit_exact(gf, world):
 
 
 def test_long_batch_without_host_sync_matches_oracle(gf):
-    """24 frames in one async batch (no host synchronisation between frames, as in the bench):
-    cross-kernel visibility of the brick state must hold whatever XCD a brick lands on."""
-    d, c, poses = _synth(24, start=40)
+    """72 frames in one async call (launches of 32 + 32 + 8 frames, no host synchronisation
+    between them, as in the bench): cross-kernel visibility of the brick state must hold whatever
+    XCD a brick lands on from one launch to the next."""
+    d, c, poses = _synth(72, start=40)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     bnds = np.array([[0.0, 10.24]] * 3)
     vol = gf.TSDFVolume(bnds.copy(), 0.08)
     orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
     vol.integrate_batch(np.ascontiguousarray(d), np.ascontiguousarray(c), K, np.linalg.inv(poses), sync=False)
-    n = sum(orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f]) for f in range(24))
+    n = sum(orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f]) for f in range(72))
     vol.sync()
     T, W, C = vol.get_state()
     assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
@@ -281,11 +282,12 @@ def test_long_batch_without_host_sync_matches_oracle(gf):
     assert vol.stats()["list_errors"] == 0
 
 
-def test_host_ingest_staging_slots_equal_device_path(gf):
-    """Frame ingest: 45 host frames (6 batches over the four staging
+def test_host_ingest_staging_slots_equal_device_path(gf, monkeypatch):
+    """Frame ingest: 45 host frames (6 batches of 8 over the four staging
     slots, two of them reused) from pageable numpy arrays and from a pinned torch tensor equal
     the device-resident run bit for bit; the call returns with the host arrays no longer needed."""
     import torch
+    monkeypatch.setenv("TSDF_BATCH", "8")  # (6 launches of 8 frames: every staging slot in turn)
     d, c, poses = _synth(45, start=5)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
     bnds = np.array([[0.0, 10.24]] * 3)
@@ -341,9 +343,10 @@ def test_prep_cull_pipeline_on_and_off_bit_identical(gf, monkeypatch, ingest):
     """u16 + RGB8 calls run as three-stage pipeline launches (k_fused: integrate batch k, cull
     k+1 and prep k+2 in one launch, three buffer sets, four staging slots; tsdf_dense.hip,
     DESIGN.md §6); TSDF_PIPELINE=0 forces the in-line prep / cull / integrate kernels.  Both
-    paths over 29 async frames (4 batches: every set and slot reused) with 65535 masking, from
+    paths over 29 async frames (4 batches of 8: every set and slot reused) with 65535 masking, from
     device and from host memory, equal each other and the oracle bit for bit."""
     import torch
+    monkeypatch.setenv("TSDF_BATCH", "8")
     d, c, poses = _synth(29, start=11)
     d = np.ascontiguousarray(d).astype(np.uint16)
     d[3:9, 50:90, 100:200] = 65535
@@ -374,7 +377,8 @@ def test_prep_cull_pipeline_on_and_off_bit_identical(gf, monkeypatch, ingest):
 
 def test_bench_workload_at_full_size_matches_oracle_rows(gf):
     """The bench's own path at BASELINE size: 512^3 @ 2 cm, 40 synthetic frames resident in HBM,
-    one async call (five batches through the three-stage k_fused launches).  22 x-rows spread
+    one async call (a full 32-frame batch and an 8-frame one through the three-stage k_fused
+    launches).  22 x-rows spread
     over the volume (every residue mod 8, so every lane column of a brick) are checked bit-exact
     against the oracle restricted to those rows; the hash path over the same frames must hold
     the same state on those rows."""

@@ -232,11 +232,12 @@ def test_hash_batch_without_host_sync_matches_dense(hf):
 def test_fused_and_inline_hash_with_growth_match_dense(hf, monkeypatch, n_shards):
     """u16 + RGB8 hash calls run as three-stage launches (k_fused_hash: integrate batch k, cull
     k+1, prep k+2; the last integrate workgroup commits the pool); TSDF_PIPELINE=0 forces the
-    in-line kernels.  20 frames in ONE synchronous call (3 batches) into a 37-slot table and a
+    in-line kernels.  20 frames in ONE synchronous call (3 batches of 8) into a 37-slot table and a
     16-block pool: both grow between batches, after the next batch's cull already ran.  Every
     path and every shard pair must equal the dense grid (bucket-range ownership is fixed at
     create, so a resize does not move blocks between shards)."""
     from tsdf_amd import grid_fusion, scene
+    monkeypatch.setenv("TSDF_BATCH", "8")
     poses = scene.trajectory(20, seed=0, start=610)
     d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=610)
     d, c = np.ascontiguousarray(d.numpy()), np.ascontiguousarray(c.numpy())

@@ -47,7 +47,7 @@ def _frames_on_device(n, start=0, ring=None):
 
 def test_config3_rank_shard_1000_frames_matches_oracle_rows():
     """One rank of config[3]: the cyclic column shard 3 of 8 of 512^3 @ 2 cm integrates 1000
-    frames (125 batches through the pipelined launches); rows at both ends of one of its columns
+    frames (32 batches of up to 32 frames through the pipelined launches); rows at both ends of one of its columns
     and inside two others equal the oracle bit for bit at the end (weights reach the hundreds)."""
     from tsdf_amd import grid_fusion, scene, sharding
     n = 1000
