@@ -375,6 +375,43 @@ def test_prep_cull_pipeline_on_and_off_bit_identical(gf, monkeypatch, ingest):
         assert _same(a, e) and _same(b, e)
 
 
+@pytest.mark.parametrize("ingest", ["device", "host"])
+def test_rgb8_gathered_in_place_equals_the_rgbx_copy(gf, monkeypatch, ingest):
+    """RGB8 frames are gathered in place (3-byte-stride buffer loads, frame_bufs) wherever the byte
+    after a frame is readable -- the padded staging slots, or a device array with more of the
+    call's frames after it; the call's last device frame goes through the prep's packed RGBX copy.
+    TSDF_RGB_DIRECT=0 forces the copy for every frame.  Both, through the fused and the in-line
+    kernels, over 19 frames (batches of 8) with colours in every byte, equal the oracle bit for bit."""
+    import torch
+    monkeypatch.setenv("TSDF_BATCH", "8")
+    d, c, poses = _synth(19, start=200)
+    rng = np.random.default_rng(3)
+    c = np.ascontiguousarray(c)
+    c[:, ::7, ::5] = rng.integers(0, 256, c[:, ::7, ::5].shape, dtype=np.uint8)  # (all byte values)
+    c[:, -1, -1] = (255, 1, 128)  # the last pixel, whose 4-byte load reaches past the frame
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    bnds = np.array([[0.0, 10.24]] * 3)
+    Tinv = np.linalg.inv(poses)
+    orc = O.OracleTSDFVolume(bnds.copy(), 0.08)
+    n = sum(orc.integrate(c[f], d[f].astype(float) / 1000.0, K, poses[f]) for f in range(len(d)))
+    for pipe in ("0", "1"):
+        for direct in ("0", "1"):
+            monkeypatch.setenv("TSDF_PIPELINE", pipe)
+            monkeypatch.setenv("TSDF_RGB_DIRECT", direct)
+            vol = gf.TSDFVolume(bnds.copy(), 0.08)
+            if ingest == "host":
+                vol.integrate_batch(np.ascontiguousarray(d), c, K, Tinv, sync=False)
+            else:
+                dd, cc = torch.from_numpy(np.ascontiguousarray(d).view(np.int16)).cuda(), torch.from_numpy(c).cuda()
+                torch.cuda.synchronize()
+                vol.integrate_batch(dd.data_ptr(), cc.data_ptr(), K, Tinv, hw=d.shape[1:], device_ptrs=True, sync=False)
+            vol.sync()
+            assert vol.stats()["voxel_updates"] == n, (pipe, direct)
+            T, W, C = vol.get_state()
+            assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu), (pipe, direct)
+            assert _same(C, orc._color_vol_cpu), (pipe, direct)
+
+
 def test_bench_workload_at_full_size_matches_oracle_rows(gf):
     """The bench's own path at BASELINE size: 512^3 @ 2 cm, 40 synthetic frames resident in HBM,
     one async call (a full 32-frame batch and an 8-frame one through the three-stage k_fused

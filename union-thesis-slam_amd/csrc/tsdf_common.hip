@@ -174,8 +174,9 @@ int Base::init(int dev, const int64_t dims[3], const int64_t off[3], const float
 }
 
 // Frames per launch (the create functions call it once, after init): sizes the per-batch buffers,
-// whose frame and cost-class dimension is the handle's batch -- 16 for a whole volume, 32 for a
-// shard -- not the kernels' capacity kMaxBatch; then buffer set 0's list and counters.
+// whose frame and cost-class dimension is the handle's batch (kFullBatch for a whole volume,
+// kMaxBatch for a shard; TSDF_BATCH overrides), not the kernels' capacity kMaxBatch; then buffer
+// set 0's list and counters.
 int Base::set_batch(int want) {
     if (const char* e = getenv("TSDF_BATCH")) want = atoi(e);
     batch = want < 1 ? 1 : want > kMaxBatch ? kMaxBatch : want;
@@ -183,6 +184,7 @@ int Base::set_batch(int want) {
     if (const char* e = getenv("TSDF_DEFER_FRAMES")) defer_frames = atoi(e);
     defer_frames = defer_frames < 1 ? 1 : defer_frames > batch ? batch : defer_frames;
     if (const char* e = getenv("TSDF_DEFER_DMA_FRAMES")) dma_grain = atoi(e) < 1 ? 1 : atoi(e);
+    if (const char* e = getenv("TSDF_RGB_DIRECT")) rgb_direct = atoi(e) != 0;  // (A/B, parity tests)
     if (list_set[0]) return TSDF_OK;
     TSDF_HIP(hipMalloc(&list_set[0], sizeof(ListEntry) * (size_t)n_bricks * batch));
     TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
@@ -452,7 +454,11 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         fr->depth_mask = mask ? dmask + npx * i : nullptr;
         fr->depth = mask ? (const void*)fr->depth_mask : fr->depth_src;
         fr->color = c + cbytes * i;
-        fr->rgbx = rgbx + npx * i;
+        // in place where the byte after the frame is readable: a staging slot (padded, stage_alloc)
+        // or a device array with more of the call's frames after this one; else the RGBX copy
+        const bool direct = ck == TSDF_COLOR_RGB8 && rgb_direct &&
+                            (!(flags & TSDF_DEVICE_PTRS) || (call_color_end && (const char*)fr->color + cbytes < call_color_end));
+        fr->rgbx = direct ? nullptr : rgbx + npx * i;
         fr->pyr = pyr + (size_t)lay.total * i;
 
         frustum_planes(fr, T, W, H);
@@ -478,7 +484,7 @@ int Base::stage_alloc(size_t dbytes, size_t cbytes) {
     st_depth_bytes = st_color_bytes = 0;
     for (int k = 0; k < kSlots; ++k) {
         TSDF_HIP(hipMalloc(&st_depth[k], dbytes * batch));
-        TSDF_HIP(hipMalloc(&st_color[k], cbytes * batch));
+        TSDF_HIP(hipMalloc(&st_color[k], cbytes * batch + 64));  // (+ the byte frame_bufs may read past the last frame)
         TSDF_HIP(hipHostMalloc(&hst_depth[k], dbytes * batch, hipHostMallocDefault));
         TSDF_HIP(hipHostMalloc(&hst_color[k], cbytes * batch, hipHostMallocDefault));
     }
@@ -530,7 +536,8 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
 }
 
 int Base::begin_call(const void* depth, size_t dbytes, const void* color, size_t cbytes, int flags) {
-    (void)depth, (void)dbytes, (void)color, (void)cbytes, (void)flags;
+    (void)depth, (void)dbytes;
+    call_color_end = (flags & TSDF_DEVICE_PTRS) ? (const char*)color + cbytes : nullptr;
     return TSDF_OK;
 }
 
@@ -542,6 +549,7 @@ int Base::end_batch(int flags, int slot) {
 
 int Base::end_call(int flags) {
     (void)flags;  // the host arrays were fully read into the bounce slots before this point
+    call_color_end = nullptr;
     return TSDF_OK;
 }
 

@@ -70,7 +70,8 @@ struct Frame {
     const void* depth_src;    // depth read by k_prep (== depth unless masking)
     unsigned short* depth_mask;  // TSDF_DEPTH_INVALID_65535: k_prep writes the masked u16 here
     const void* color;        // the caller's colour (RGB8 or folded f32)
-    const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (k_pyramid writes it)
+    const unsigned* rgbx;     // RGB8 packed r | g<<8 | b<<16 per pixel (the prep writes it), or
+                              // null: the integrate gathers the caller's RGB8 itself (frame_bufs)
     const float* pyr;         // max-depth pyramid (metres), levels 1..6 concatenated
     float planes[5][4];       // half-spaces n.q + d >= 0 containing every valid voxel, q = world
                               // point - eye (cull; camera-relative, so f32 stays accurate for
@@ -455,7 +456,14 @@ __device__ inline FrameBufs frame_bufs(const Frame& fr) {
     const int n = fr.W * fr.H;
     FrameBufs b;
     b.depth = __builtin_amdgcn_make_buffer_rsrc((void*)fr.depth, DK == 0 ? 2 : 8, n, kBufDword3);
-    b.color = __builtin_amdgcn_make_buffer_rsrc((void*)(CK == 0 ? (const void*)fr.rgbx : fr.color), 4, n, kBufDword3);
+    // RGB8 (CK == 0): a 4-byte load at pixel p of a 3-byte-stride structured buffer returns r, g, b in
+    // bytes 0-2 (the integrate decodes those three; the range check is on the pixel index), so the
+    // caller's frame is gathered as it lies -- provided the byte after its last pixel is readable
+    // (prepare_batch: the call's array or the padded staging slot goes on); otherwise the prep's
+    // packed RGBX copy (round 5: dense +1.0 %, hash +1.6 %, eighth shards +2.9 % / +5.8 %,
+    // profiles/r05_rgb_direct/)
+    if (CK == 0 && !fr.rgbx) b.color = __builtin_amdgcn_make_buffer_rsrc((void*)fr.color, 3, n, kBufDword3);
+    else b.color = __builtin_amdgcn_make_buffer_rsrc((void*)(CK == 0 ? (const void*)fr.rgbx : fr.color), 4, n, kBufDword3);
     return b;
 }
 template <int DK>
@@ -1525,10 +1533,12 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
                 ma = fmaxf(ma, fmaxf((float)(dd.x & 0xFFFFu) * 1e-3f, (float)(dd.x >> 16) * 1e-3f));
                 mb = fmaxf(mb, fmaxf((float)(dd.y & 0xFFFFu) * 1e-3f, (float)(dd.y >> 16) * 1e-3f));
             }
-            const unsigned* q = (const unsigned*)((const unsigned char*)fr.color + 3 * p);
-            const unsigned a = q[0], b = q[1], cc = q[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
-            *(uint4*)((unsigned*)fr.rgbx + p) =
-                make_uint4(a & 0xFFFFFFu, (a >> 24) | ((b & 0xFFFFu) << 8), (b >> 16) | ((cc & 0xFFu) << 16), cc >> 8);
+            if (fr.rgbx) {  // (frames the integrate cannot gather in place, frame_bufs)
+                const unsigned* q = (const unsigned*)((const unsigned char*)fr.color + 3 * p);
+                const unsigned a = q[0], b = q[1], cc = q[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+                *(uint4*)((unsigned*)fr.rgbx + p) =
+                    make_uint4(a & 0xFFFFFFu, (a >> 24) | ((b & 0xFFFFu) << 8), (b >> 16) | ((cc & 0xFFu) << 16), cc >> 8);
+            }
         }
     }
     const PyrGeo& pg = bt.pg;
@@ -1607,7 +1617,7 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
                 } else {
                     d = (float)((const double*)fr.depth_src)[p];
                 }
-                if (CK == 0) {
+                if (CK == 0 && rgbx) {
                     const unsigned char* q = (const unsigned char*)fr.color + 3 * (size_t)p;
                     rgbx[p] = (unsigned)q[0] | ((unsigned)q[1] << 8) | ((unsigned)q[2] << 16);
                 }

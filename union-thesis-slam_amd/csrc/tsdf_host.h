@@ -75,10 +75,14 @@ struct Base {
     int set_batch(int want);  // (tsdf_common.hip: also allocates buffer set 0's list)
     // frames a deferred per-frame batch collects (TSDF_DEFER) before it runs: 8 -- the host's
     // frame copies of the next batch overlap the ingest and integrate of this one at a finer
-    // grain than a whole launch's 16 frames (TSDF_DEFER_FRAMES overrides)
+    // grain than a whole launch's 32 frames (TSDF_DEFER_FRAMES overrides)
     int defer_frames = 8;
     // deferred frames whose DMA is issued together while the batch fills (TSDF_DEFER_DMA_FRAMES)
     int dma_grain = 2;
+    // RGB8 frames gathered in place by the integrate (frame_bufs) where the byte after a frame is
+    // readable, instead of through the prep's RGBX copy (TSDF_RGB_DIRECT=0: always the copy)
+    bool rgb_direct = true;
+    const char* call_color_end = nullptr;  // end of the current call's device colour array (begin_call)
     // Per-batch buffers of the CURRENT buffer set (use_set).
     float* pyr = nullptr;      // `batch` per-frame max-depth pyramids
     unsigned* rgbx = nullptr;  // `batch` per-frame packed RGB8 images
@@ -116,7 +120,7 @@ struct Base {
 
     // Deferred single frames (TSDF_DEFER, the reference's one-integrate()-per-frame call
     // pattern): each call copies its frame straight into bounce slot `slot` and returns; every
-    // kMaxBatch frames (or at any other call on the handle) the collected frames run as one
+    // defer_frames frames (or at any other call on the handle) the collected frames run as one
     // asynchronous batch -- temporal batching for per-frame callers, same results.
     struct Deferred {
         int n = 0, H = 0, W = 0, dk = 0, ck = 0, slot = -1;
