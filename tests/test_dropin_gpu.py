@@ -25,9 +25,10 @@ def _synth(n, start=0):
 
 
 def test_deferred_per_frame_integrate_matches_oracle():
-    """19 per-frame calls with f64 metres (half of them not millimetre-exact), varying
-    obs_weight, a change of intrinsics mid-stream and reads in between (each read runs the
-    pending frames first): deferred, undeferred and the oracle agree bit for bit."""
+    """19 per-frame calls with f64 metres (half of them not millimetre-exact, so deferred batches
+    staged as u16 millimetres are flushed early by a frame that stays f64), varying obs_weight, a
+    change of intrinsics mid-stream and reads in between (each read runs the pending frames
+    first): deferred, undeferred and the oracle agree bit for bit."""
     from tsdf_amd import grid_fusion
     d, c, poses = _synth(19, start=333)
     K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
@@ -53,6 +54,32 @@ def test_deferred_per_frame_integrate_matches_oracle():
     assert dv.stats()["voxel_updates"] == nv.stats()["voxel_updates"] == n_orc
     for a, b, o in zip(dv.get_state(), nv.get_state(), (orc._tsdf_vol_cpu, orc._weight_vol_cpu, orc._color_vol_cpu)):
         assert _same(a, o) and _same(b, o)
+
+
+@pytest.mark.parametrize("mm", ["1", "0"])
+def test_deferred_millimetre_metres_staged_as_u16(monkeypatch, mm):
+    """The demos' depth (png / 1000.: every value RN(k / 1000)) is staged as u16 millimetres by the
+    deferred per-frame calls (a quarter of the bytes over PCIe; TSDF_DEFER_MM=0 stages the f64 as
+    it comes): 20 frames -- two full deferred batches and a flushed partial one -- equal the oracle
+    bit for bit either way, and the hash table equals the dense grid."""
+    from tsdf_amd import grid_fusion, hash_fusion
+    monkeypatch.setenv("TSDF_DEFER_MM", mm)
+    d, c, poses = _synth(20, start=470)
+    K = np.array([[585.0, 0, 320], [0, 585.0, 240], [0, 0, 1]])
+    dv = grid_fusion.TSDFVolume(np.array(BNDS), 0.08)
+    hv = hash_fusion.HashTable(np.array(BNDS), 0.08)
+    orc = O.OracleTSDFVolume(np.array(BNDS), 0.08)
+    n = 0
+    for f in range(20):
+        m = d[f].astype(float) / 1000.0
+        dv.integrate(c[f], m, K, poses[f])
+        hv.integrate(c[f], m, K, poses[f])
+        n += orc.integrate(c[f], m, K, poses[f])
+    T, W, C = dv.get_state()
+    assert _same(T, orc._tsdf_vol_cpu) and _same(W, orc._weight_vol_cpu) and _same(C, orc._color_vol_cpu)
+    assert dv.stats()["voxel_updates"] == n
+    for a, b in zip(dv.get_state(), hv.get_state()):  # (the hash equals the dense grid)
+        assert np.array_equal(a, b)
 
 
 def test_deferred_hash_per_frame_matches_dense():

@@ -1,5 +1,6 @@
 """Per-frame integrate() rate from host NumPy (the reference's call pattern), several passes, for
-A/B of the host copy path (TSDF_COPY_THREADS):  python tools/gpu/dropin_rate.py [frames] [passes]"""
+A/B of the host copy path (TSDF_COPY_THREADS):  python tools/gpu/dropin_rate.py [frames] [passes]
+[TSDF_DEFER_MM values, e.g. 1,0: each measured in turn, twice, on fresh handles]"""
 import json
 import os
 import sys
@@ -8,7 +9,9 @@ import time
 import numpy as np
 import torch
 
-from tsdf_amd import grid_fusion, hash_fusion, scene
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                "union-thesis-slam_amd"))
+from tsdf_amd import grid_fusion, hash_fusion, scene  # noqa: E402
 
 
 def main():
@@ -21,21 +24,27 @@ def main():
     ch = c.cpu().numpy()
     K = scene.intrinsics()
     out = {"copy_threads": os.environ.get("TSDF_COPY_THREADS", "default")}
-    for name, mk in (("dense", lambda: grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.02)),
-                     ("hash", lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
-                                                            max_blocks=1 << 15))):
-        v = mk()
-        v.integrate(ch[0], d64[0], K, poses[0])
-        v.sync()
-        rates = []
-        for _ in range(passes):
-            t0 = time.perf_counter()
-            for i in range(nd):
-                v.integrate(ch[i], d64[i], K, poses[i])
-            v.sync()
-            rates.append(round(nd / (time.perf_counter() - t0), 1))
-        out[name] = rates
-        v.close()
+    modes = sys.argv[3].split(",") if len(sys.argv) > 3 else [None]
+    for rep in range(2 if modes[0] is not None else 1):
+        for mode in modes:
+            if mode is not None:
+                os.environ["TSDF_DEFER_MM"] = mode  # (read when a handle is created)
+            for name, mk in (("dense", lambda: grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.02)),
+                             ("hash", lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
+                                                                    max_blocks=1 << 15))):
+                v = mk()
+                v.integrate(ch[0], d64[0], K, poses[0])
+                v.sync()
+                rates = []
+                for _ in range(passes):
+                    t0 = time.perf_counter()
+                    for i in range(nd):
+                        v.integrate(ch[i], d64[i], K, poses[i])
+                    v.sync()
+                    rates.append(round(nd / (time.perf_counter() - t0), 1))
+                key = name if mode is None else f"{name}_mm{mode}_rep{rep}"
+                out[key] = rates
+                v.close()
     print(json.dumps(out))
 
 

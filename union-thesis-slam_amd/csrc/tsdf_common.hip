@@ -185,6 +185,7 @@ int Base::set_batch(int want) {
     defer_frames = defer_frames < 1 ? 1 : defer_frames > batch ? batch : defer_frames;
     if (const char* e = getenv("TSDF_DEFER_DMA_FRAMES")) dma_grain = atoi(e) < 1 ? 1 : atoi(e);
     if (const char* e = getenv("TSDF_RGB_DIRECT")) rgb_direct = atoi(e) != 0;  // (A/B, parity tests)
+    if (const char* e = getenv("TSDF_DEFER_MM")) defer_mm = atoi(e) != 0;
     if (list_set[0]) return TSDF_OK;
     TSDF_HIP(hipMalloc(&list_set[0], sizeof(ListEntry) * (size_t)n_bricks * batch));
     TSDF_HIP(hipMalloc(&count_set[0], sizeof(unsigned int) * kCountWords));
@@ -273,12 +274,37 @@ static void frustum_planes(Frame* fr, const double* T, int W, int H) {
     }
 }
 
-// memcpy with up to 8 threads (host bounce copies run at several times one core's bandwidth)
+// f64 metres -> u16 millimetres where that is exact: every d must be RN(k / 1000) for an integer k
+// in [0, 65535] -- what the demos' depth_im = png / 1000. holds -- checked by recomputing it as the
+// kernels' u16 path does, fma(k, 0.001, k * C_LO) (exact for every u16, tools/check_depth_conversion.c),
+// so the integrate sees the same metres either way; NaN, negatives, other values fail.  Returns
+// whether all n did (dst is then complete).  -0.0 passes as 0, which every use of depth treats alike
+// (depth > 0 and depth - z).
+static inline bool depth_mm_range(unsigned short* dst, const double* src, size_t n) {
+    unsigned bad = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const double d = src[i];
+        const double k = fmin(fmax(__builtin_rint(d * 1000.0), 0.0), 65535.0);  // (NaN -> 0)
+        const double back = __builtin_fma(k, 0.001, k * -2.0858186326137145e-20);
+        bad |= (unsigned)(back != d);
+        dst[i] = (unsigned short)(int)k;
+    }
+    return bad == 0;
+}
+__attribute__((target("avx2,fma"))) static bool depth_mm_avx2(unsigned short* dst, const double* src, size_t n) {
+    return depth_mm_range(dst, src, n);
+}
+static bool depth_mm_any(unsigned short* dst, const double* src, size_t n) {
+    static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+    return avx2 ? depth_mm_avx2(dst, src, n) : depth_mm_range(dst, src, n);
+}
+
 // Host copies into the page-locked bounce slots (ingest and the deferred drop-in frames) by a
 // persistent pool of copy threads: one 640x480 f64 depth frame is 2.4 MB, and a single-thread
 // memcpy of it and its colour (~140 us) bounded the per-frame drop-in rate (6k frames/s; 10k
 // with the pool); spawning threads per call cost more than it saved below 4 MB.  The caller copies one share itself; the workers wake
 // on a generation counter.  TSDF_COPY_THREADS sets the pool size (0: copy on the calling thread).
+// The pool also runs the deferred frames' depth conversion (depth_mm_any), share by share.
 namespace {
 class CopyPool {
   public:
@@ -295,25 +321,48 @@ class CopyPool {
             std::memcpy(dst, src, bytes);
             return;
         }
-        std::lock_guard<std::mutex> call(call_);  // one copy at a time through the pool
+        run_job(0, dst, src, bytes, 64);
+    }
+    bool depth_mm(unsigned short* dst, const double* src, size_t n) {  // depth_mm_any over the pool
+        if (workers_.empty() || n < (32u << 10)) return depth_mm_any(dst, src, n);
+        bad_ = 0;
+        run_job(1, dst, src, n, 64);
+        return bad_ == 0;
+    }
+
+  private:
+    // job 0: copy `n` bytes; job 1: convert `n` depth values; shares of `chunk` units (a multiple
+    // of `align`), share 0 on the calling thread
+    void run_job(int job, void* dst, const void* src, size_t n, size_t align) {
+        const int nw = (int)workers_.size();
+        std::lock_guard<std::mutex> call(call_);  // one job at a time through the pool
         const size_t parts = (size_t)nw + 1;
-        const size_t chunk = ((bytes + parts - 1) / parts + 63) & ~(size_t)63;
+        const size_t chunk = ((n + parts - 1) / parts + align - 1) / align * align;
         {
             std::lock_guard<std::mutex> g(m_);
+            job_ = job;
             dst_ = (char*)dst;
             src_ = (const char*)src;
-            bytes_ = bytes;
+            bytes_ = n;
             chunk_ = chunk;
             left_ = nw;
             ++gen_;
         }
         cv_.notify_all();
-        std::memcpy(dst, src, std::min(chunk, bytes));  // share 0 on the calling thread
+        share(job, (char*)dst, (const char*)src, n, chunk, 0);
         std::unique_lock<std::mutex> g(m_);
         done_.wait(g, [&] { return left_ == 0; });
     }
-
-  private:
+    void share(int job, char* d, const char* s, size_t n, size_t chunk, int k) {
+        const size_t o = (size_t)k * chunk;
+        if (o >= n) return;
+        const size_t len = std::min(chunk, n - o);
+        if (job == 0) {
+            std::memcpy(d + o, s + o, len);
+        } else if (!depth_mm_any((unsigned short*)d + o, (const double*)s + o, len)) {
+            bad_ = 1;
+        }
+    }
     CopyPool() : pid_(getpid()) {
         // two workers (three shares): 12.3k frames/s per-frame dense drop-in against 7.2k on the
         // calling thread alone; four or eight were no faster and dipped more often
@@ -323,20 +372,20 @@ class CopyPool {
         for (int i = 0; i < n; ++i) workers_.emplace_back([this, i] { run(i + 1); });
         for (auto& t : workers_) t.detach();  // live for the process
     }
-    void run(int share) {
+    void run(int k) {
         unsigned long long seen = 0;
         for (;;) {
+            int job;
             char* d;
             const char* s;
-            size_t bytes, chunk;
+            size_t n, chunk;
             {
                 std::unique_lock<std::mutex> g(m_);
                 cv_.wait(g, [&] { return gen_ != seen; });
                 seen = gen_;
-                d = dst_, s = src_, bytes = bytes_, chunk = chunk_;
+                job = job_, d = dst_, s = src_, n = bytes_, chunk = chunk_;
             }
-            const size_t o = (size_t)share * chunk;
-            if (o < bytes) std::memcpy(d + o, s + o, std::min(chunk, bytes - o));
+            share(job, d, s, n, chunk, k);
             std::lock_guard<std::mutex> g(m_);
             if (--left_ == 0) done_.notify_one();
         }
@@ -345,13 +394,22 @@ class CopyPool {
     std::vector<std::thread> workers_;
     std::mutex call_, m_;
     std::condition_variable cv_, done_;
+    int job_ = 0;
     char* dst_ = nullptr;
     const char* src_ = nullptr;
     size_t bytes_ = 0, chunk_ = 0;
     int left_ = 0;
     unsigned long long gen_ = 0;
+    std::atomic<int> bad_{0};
 };
 }  // namespace
+
+// (diagnostic / CPU tests, not in the header) the deferred frames' f64 -> u16 depth conversion:
+// 1 if all n values converted exactly, else 0
+extern "C" int tsdf_diag_depth_to_mm(const double* src, long long n, unsigned short* dst) {
+    if (!src || !dst || n < 0) return set_error(TSDF_E_ARG, "bad arguments");
+    return CopyPool::get().depth_mm(dst, src, (size_t)n) ? 1 : 0;
+}
 
 static void par_memcpy(void* dst, const void* src, size_t bytes) {
     if (bytes < (4u << 20)) {  // one frame (the drop-in's deferred frames): the pool
@@ -494,18 +552,19 @@ int Base::stage_alloc(size_t dbytes, size_t cbytes) {
 }
 
 bool Base::defer_same(int dk, int ck, int H, int W, const double* K) const {
-    return dfr.dk == dk && dfr.ck == ck && dfr.H == H && dfr.W == W && std::memcmp(dfr.K, K, sizeof(dfr.K)) == 0;
+    return dfr.dk_in == dk && dfr.ck == ck && dfr.H == H && dfr.W == W && std::memcmp(dfr.K, K, sizeof(dfr.K)) == 0;
 }
 
 int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H, int W,
                      const double* K, const double* T, double ow) {
-    const size_t dbytes = frame_bytes_depth(dk, H, W), cbytes = frame_bytes_color(ck, H, W);
+    const size_t cbytes = frame_bytes_color(ck, H, W), npx = (size_t)H * W;
     if (dfr.n == 0) {
-        TSDF_TRY(stage_alloc(dbytes, cbytes));
+        TSDF_TRY(stage_alloc(frame_bytes_depth(dk, H, W), cbytes));  // (sized for the caller's kind)
         dfr.slot = defer_next;
         dfr.copied = 0;
         defer_next = (defer_next + 1) % kSlots;
         TSDF_HIP(hipEventSynchronize(ev_copied[dfr.slot]));  // its previous DMA has finished
+        dfr.dk_in = dk;
         dfr.dk = dk;
         dfr.ck = ck;
         dfr.H = H;
@@ -513,7 +572,23 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
         std::memcpy(dfr.K, K, sizeof(dfr.K));
     }
     const int i = dfr.n;
-    par_memcpy((char*)hst_depth[dfr.slot] + dbytes * i, depth, dbytes);
+    // f64 metres that are all RN(k / 1000) -- the demos' png / 1000. -- go as u16 millimetres: a
+    // quarter of the bytes into the bounce slot and over PCIe, the same metres in the kernels
+    // (depth_mm_any); a batch holds one kind, so a frame that does not convert after u16 ones
+    // sends the caller back to flush them first (kDeferFlush), and then starts an f64 batch
+    bool staged = false;
+    if (dk == TSDF_DEPTH_F64_M && defer_mm && (i == 0 || dfr.dk == TSDF_DEPTH_U16_MM)) {
+        if (CopyPool::get().depth_mm((unsigned short*)hst_depth[dfr.slot] + npx * i, (const double*)depth, npx)) {
+            dfr.dk = TSDF_DEPTH_U16_MM;
+            staged = true;
+        } else if (i > 0) {
+            return kDeferFlush;
+        } else {
+            dfr.dk = TSDF_DEPTH_F64_M;
+        }
+    }
+    const size_t dbytes = frame_bytes_depth(dfr.dk, H, W);
+    if (!staged) par_memcpy((char*)hst_depth[dfr.slot] + dbytes * i, depth, dbytes);
     par_memcpy((char*)hst_color[dfr.slot] + cbytes * i, color, cbytes);
     std::memcpy(dfr.T + 16 * i, T, 16 * sizeof(double));
     dfr.ow[i] = ow;

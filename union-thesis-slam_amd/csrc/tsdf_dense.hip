@@ -399,7 +399,12 @@ int tsdf_dense_integrate(tsdf_dense_t* h, const void* depth, int depth_kind, con
     if (flags & TSDF_DEFER) {
         if (flags & TSDF_DEVICE_PTRS) return set_error(TSDF_E_ARG, "TSDF_DEFER takes host frames only");
         if (B.dfr.n > 0 && !B.defer_same(depth_kind, color_kind, height, width, K)) TSDF_TRY(dense_flush(h));
-        TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, obs_weight));
+        int r = B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, obs_weight);
+        if (r == Base::kDeferFlush) {  // the batch's frames went as u16 and this one cannot
+            TSDF_TRY(dense_flush(h));
+            r = B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, obs_weight);
+        }
+        TSDF_TRY(r);
         if (B.dfr.n == B.defer_frames) TSDF_TRY(dense_flush(h));
         return TSDF_OK;
     }

@@ -1398,7 +1398,12 @@ int tsdf_hash_integrate(tsdf_hash_t* h, const void* depth, int depth_kind, const
         // a pending batch's re-run reads its staging slots: settle it before they are reallocated
         if (h->pend.on && !B.stage_fits(depth_kind, color_kind, height, width)) TSDF_TRY(hash_settle(h));
         // HashTable.integrate ignores obs_weight (hash_fusion.py:141,145): always 1
-        TSDF_TRY(B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0));
+        int r = B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0);
+        if (r == Base::kDeferFlush) {  // the batch's frames went as u16 and this one cannot
+            TSDF_TRY(hash_flush(h));
+            r = B.defer_push(depth, depth_kind, color, color_kind, height, width, K, world_to_cam, 1.0);
+        }
+        TSDF_TRY(r);
         if (B.dfr.n == B.defer_frames) TSDF_TRY(hash_flush(h, false));
         return TSDF_OK;
     }

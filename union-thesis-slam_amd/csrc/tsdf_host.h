@@ -82,6 +82,9 @@ struct Base {
     // RGB8 frames gathered in place by the integrate (frame_bufs) where the byte after a frame is
     // readable, instead of through the prep's RGBX copy (TSDF_RGB_DIRECT=0: always the copy)
     bool rgb_direct = true;
+    // deferred f64-metre frames that are all RN(k / 1000) staged as u16 millimetres (defer_push;
+    // TSDF_DEFER_MM=0: as they come)
+    bool defer_mm = true;
     const char* call_color_end = nullptr;  // end of the current call's device colour array (begin_call)
     // Per-batch buffers of the CURRENT buffer set (use_set).
     float* pyr = nullptr;      // `batch` per-frame max-depth pyramids
@@ -124,6 +127,7 @@ struct Base {
     // asynchronous batch -- temporal batching for per-frame callers, same results.
     struct Deferred {
         int n = 0, H = 0, W = 0, dk = 0, ck = 0, slot = -1;
+        int dk_in = 0;   // the callers' depth kind (dk: as staged -- u16 for f64 metres that convert exactly)
         int copied = 0;  // frames whose DMA to the device staging slot is already issued
         double K[9];
         double T[16 * kMaxBatch];
@@ -133,8 +137,10 @@ struct Base {
     int prestaged = -1;   // >= 0: the call's (single) batch already sits in this bounce slot
     int pre_copied = 0;   // ... and its first pre_copied frames are already on their way to the device
     bool defer_same(int dk, int ck, int H, int W, const double* K) const;
+    // returns kDeferFlush when the frame cannot join the batch's kind: flush, then push it again
     int defer_push(const void* depth, int dk, const void* color, int ck, int H, int W,
                    const double* K, const double* T, double ow);
+    static constexpr int kDeferFlush = 1;
     int stage_alloc(size_t dbytes, size_t cbytes);  // bounce + device staging slots (per frame)
     bool stage_fits(int dk, int ck, int H, int W) const {  // frames of this size need no reallocation
         return st_depth_bytes >= frame_bytes_depth(dk, H, W) * batch &&
