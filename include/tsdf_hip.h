@@ -49,10 +49,12 @@ extern "C" {
 #define TSDF_DEFER 8        /* tsdf_*_integrate (host frames only): copy the frame into a pinned
                                staging batch and return; the batch runs (asynchronously, as one
                                temporally batched launch) once it holds 8 frames
-                               (TSDF_DEFER_FRAMES overrides; half a 16-frame launch,
-                               the host's copy grain) or at the next other call
+                               (TSDF_DEFER_FRAMES overrides; a quarter of a 32-frame
+                               launch, the host's copy grain) or at the next other call
                                on the handle -- the reference's one-integrate()-per-
                                frame loop (grid_demo1.py:76-87) at batched speed, same results.
+                               f64-metre depth whose every value is exactly RN(k / 1000),
+                               k < 65536 integer (png / 1000.), is staged as u16 millimetres.
                                Hash: a full table / pool found after a deferred batch is grown
                                and its skipped bricks re-run at the next call, before anything
                                else runs (exact, as for synchronous calls) */
