@@ -19,7 +19,7 @@ so total work is fixed: "scaling": "strong".
 Rank 0 prints ONE JSON line.  `roofline` prices the integrate launch by SURVEY §8(d)'s bytes with
 temporal batching accounted for (24 B per voxel the launch's batch updates at least once, counted
 on the device, + 5 B per pixel per frame) over its HIP-event time, so it cannot pass 1 by batching;
-the hash leg carries the same block (+ 16 B per touched block);
+the hash leg carries the same block (+ 16 B per block looked up);
 `cpu_baseline` is the NumPy restatement of the reference's CPU path (oracle/, pinned to the
 reference fixtures) on a bounded sample, with the host's CPU model and BLAS threads.
 Beside `value`: the hash path, the PCIe-inclusive batch rate, the reference's own per-frame
@@ -50,11 +50,11 @@ WORKLOAD = "config[1]: 640x480 synthetic frames (bench ring, mean V_f 11.7%) int
 # the committed PMC passes of this round's kernel (tools/gpu/run_round_prof.sh), quoted only when
 # their workload AND the build id of the library they measured match the loaded library
 # (tsdf_build_id): DRAM-side traffic (FETCH_SIZE / WRITE_SIZE) and VALU issue (SQ counters)
-PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r05.json")
-SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r05.json")
+PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r06.json")
+SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r06.json")
 HASH_WORKLOAD = ("config[2]: the same frames into a voxel hash over the 512^3 @ 2 cm extent (8^3 blocks, 2^22 "
                  "slots, pool grown from 2^15 blocks)")
-HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r05.json")  # traffic + SQ of k_fused_hash<0, true>
+HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r06.json")  # traffic + SQ of k_fused_hash<0, true>
 
 
 def log(*a):
@@ -132,19 +132,25 @@ def attach_profiles(roof, st, build_id, pmc_path, sq_path, workload):
             why.append(f"{key}: {rel} measured library build {p.get('build_id')}, this is {build_id}")
             continue
         avg_s = roof["kernel_avg_us"] / 1e6
-        if key == "traffic" and p.get("hbm_bytes_per_launch"):
-            tb = float(p["hbm_bytes_per_launch"])
+        if key == "traffic" and p.get("l2_memside_bytes_per_launch"):
+            tb = float(p["l2_memside_bytes_per_launch"])
             roof["traffic"] = round(tb)
             # measured L2 memory-side bytes over this run's average launch time
             roof["traffic_frac"] = round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             roof["traffic_over_algorithmic"] = round(tb / roof["bytes_per_launch"], 3)
-            roof["traffic_source"] = (rel + " (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH "
-                                      "doubled per the gfx950 rule; build " + build_id + ")")
-            roof["traffic_note"] = ("FETCH/WRITE_SIZE count the L2's memory-side requests, Infinity-Cache (256 MB) "
-                                    "hits included: the excess over the algorithmic bytes is the frames' depth / "
-                                    "colour gathers refetched into the 4 MB per-XCD L2s by every brick projecting "
-                                    "onto them (a launch's 32 frames of images, ~60 MB, stay in the Infinity "
-                                    "Cache), not DRAM re-reads that a counter could separate (DESIGN.md §4)")
+            if p.get("raw_bytes_per_launch"):
+                roof["traffic_raw"] = round(float(p["raw_bytes_per_launch"]))
+            if p.get("read_requests_median"):
+                roof["traffic_read_requests"] = p["read_requests_median"]
+            roof["traffic_source"] = (rel + " (separate rocprofv3 --pmc passes of the same build " + build_id +
+                                      ": reads = the L2's memory-side read requests by size, 32 / 64 / 128 B "
+                                      "(TCC_EA0_RDREQ_*B; FETCH_SIZE tallies a 128-B request at 64 B: traffic_raw "
+                                      "= FETCH_SIZE + WRITE_SIZE as reported); writes = WRITE_SIZE)")
+            roof["traffic_note"] = ("L2 memory-side traffic, Infinity-Cache (256 MB) hits included, so an upper bound "
+                                    "on DRAM bytes; its excess over the algorithmic bytes is the frames' depth / "
+                                    "colour gathers refilled into the 4 MB per-XCD L2s by the bricks projecting "
+                                    "onto them (a launch's 32 frames of images, ~48 MB, fit the Infinity Cache; "
+                                    "DESIGN.md §4)")
         med = p.get("median_per_launch", {})
         if key == "valu" and med.get("SQ_INSTS_VALU"):
             vox_launch = st["voxel_updates"] / st["kernel_launches"]
@@ -172,8 +178,9 @@ def integrate_roofline(st, frames, kernel, first_timed=None, blocks_touched=None
     """HBM roofline of the integrate launches, priced by the bytes a launch must
     move: each voxel its batch updates at least once is read and written once (24 B: tsdf, weight,
     colour f32 in and out -- temporal batching keeps it on chip across the batch's frames), plus
-    5 B per pixel per frame of input (u16 depth + RGB8), plus for the hash 16 B per touched block
-    (key + slot value).  Counted on the device (tsdf_stats_t.batch_voxels), so `frac` cannot pass
+    5 B per pixel per frame of input (u16 depth + RGB8), plus for the hash 16 B per block its cull
+    looks up (key + slot value: one probe per kept block per launch -- a per-block count; the
+    stats' bricks_touched counts z-half waves).  Counted on the device (tsdf_stats_t.batch_voxels), so `frac` cannot pass
     1 by batching.  `per_frame_bytes_frac` keeps the per-frame pricing (24 B per update per frame)
     as a secondary figure: the state traffic batching avoids."""
     if not st["kernel_launches"]:
@@ -191,7 +198,9 @@ def integrate_roofline(st, frames, kernel, first_timed=None, blocks_touched=None
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "traffic_frac": None,
             "kernel": kernel,
             "bytes_rule": "24 B x U_batch (voxels updated at least once per launch, counted on the device) + "
-                          "5 B x pixels x frames" + (" + 16 B x touched brick halves" if blocks_touched is not None else ""),
+                          "5 B x pixels x frames" + (" + 16 B x blocks looked up (one key + slot-value probe per "
+                                                     "kept block per launch, by its cull)"
+                                                     if blocks_touched is not None else ""),
             "kernel_avg_us": round(1e6 * avg_s, 2),
             "bytes_per_launch": round(alg / L),
             "batch_voxels_per_launch": round(st["batch_voxels"] / L),
@@ -581,7 +590,7 @@ def main():
         hroof = integrate_roofline(hs, Kf, "tsdf::k_fused_hash<0, true>: integrates batch k (find-or-insert of its "
                                            "blocks), culls k+1 and preps k+2 in the same launch; the window "
                                            "inserts blocks_allocated_in_window blocks",
-                                   blocks_touched=hs["bricks_touched"])
+                                   blocks_touched=hs["lookups"])
         if hroof is not None:
             attach_profiles(hroof, hs, _ffi.build_id(), HASH_PROFILE, HASH_PROFILE, HASH_WORKLOAD)
             hash_res["roofline"] = hroof

@@ -397,3 +397,56 @@ def test_trim_integrate_trim_integrate_stays_exact():
     assert h.info()["pool_mapped"] == 1
     for a, b in zip(g.get_state(), h.get_state()):
         assert np.array_equal(a, b)
+
+
+def test_long_per_frame_hash_run_doubles_only_with_its_keys():
+    """Round-5 verdict item 4: 2048 per-frame deferred calls (256 bench-ring frames, f64 metres,
+    cycled 8 times) into a table of 2^10 at 4 cm.  Every 8-frame batch ends by freeing the blocks
+    its cull inserted for bricks no frame updated -- tombstones where the next slot is taken -- so
+    over the run the table sees thousands of them.  The table must double only as its live keys
+    require (needs_resize / double_table_size, hash_fusion.py:156-161,414-437): the last doubling
+    was due when the live keys reached 0.75 of the size before it; tombstones are purged by
+    same-size rebuilds and stay within the policy's limit.  The state equals the dense grid."""
+    import torch
+    from tsdf_amd import grid_fusion, hash_fusion, scene
+    n, cycles = 256, 8
+    poses = scene.trajectory(n, seed=0, radius_frac=scene.BENCH_RING)
+    dd, cc = scene.render(poses, scene.make_spheres(0, ring_frac=scene.BENCH_RING), seed=0,
+                          device=torch.device("cuda", 0), depth_dtype=torch.int16)
+    d = np.ascontiguousarray(dd.cpu().numpy().view(np.uint16))
+    c = np.ascontiguousarray(cc.cpu().numpy())
+    del dd, cc
+    K = scene.intrinsics()
+    m = d.astype(np.float64) / 1000.0  # as grid_demo1.py:81 (millimetre-exact: staged as u16)
+    s0 = 1 << 10
+    h = hash_fusion.HashTable(np.array(BNDS), 0.04, s0, max_blocks=1 << 10)
+    caps = [s0]
+    live_at_doubling = []
+    for k in range(cycles):
+        for f in range(n):
+            h.integrate(c[f], m[f], K, poses[f])
+            if f % 64 == 63:
+                i = h.info()
+                if i["capacity"] != caps[-1]:
+                    caps.append(int(i["capacity"]))
+                    live_at_doubling.append(int(i["used"]))
+    h.sync()
+    info = h.info()
+    ms, live = int(info["capacity"]), int(info["used"])
+    # the policy's size for the run's keys: the start size doubled while live >= 0.75 of it (the
+    # keys at a check include the batch's not-yet-freed inserts: up to a few hundred more)
+    need = s0
+    while live >= 0.75 * need:
+        need *= 2
+    assert ms in (need, 2 * need), (ms, need, live, caps)
+    if ms == 2 * need:  # only if the transient inserts crossed the threshold at a check
+        assert live + 2048 >= 0.75 * need, (ms, need, live)
+    # doublings happen only during the first pass over the frames (afterwards no new keys)
+    assert len(caps) - 1 == int(round(np.log2(ms / s0)))
+    assert info["tombstones"] + live < 0.75 * ms + 2048, info  # purged, within one call's frees
+    g = grid_fusion.TSDFVolume(np.array(BNDS), 0.04)
+    Tinv = np.linalg.inv(poses)
+    for k in range(cycles):
+        g.integrate_batch(d, c, K, Tinv)
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)

@@ -29,7 +29,8 @@ def _roof():
 def _profiles(tmp_path, build, workload):
     pmc = tmp_path / "pmc.json"
     sq = tmp_path / "sq.json"
-    pmc.write_text(json.dumps({"build_id": build, "workload": workload, "hbm_bytes_per_launch": 2.2e9}))
+    pmc.write_text(json.dumps({"build_id": build, "workload": workload, "l2_memside_bytes_per_launch": 2.2e9,
+                               "raw_bytes_per_launch": 1.3e9}))
     sq.write_text(json.dumps({"build_id": build, "workload": workload, "valu_busy_per_simd": 0.88,
                               "median_per_launch": {"SQ_INSTS_VALU": 3.4e8}}))
     return str(pmc), str(sq)
@@ -40,7 +41,7 @@ def test_profiles_attach_only_for_the_same_build_and_workload(bench, tmp_path, m
     pmc, sq = _profiles(tmp_path, "abc", bench.WORKLOAD)
     roof = _roof()
     bench.attach_profiles(roof, st, "abc", pmc, sq, bench.WORKLOAD)
-    assert roof["traffic"] == 2_200_000_000 and roof["bound"] == "valu"
+    assert roof["traffic"] == 2_200_000_000 and roof["bound"] == "valu" and roof["traffic_raw"] == 1_300_000_000
     assert roof["traffic_over_algorithmic"] == pytest.approx(2.2e9 / 1.95e9, abs=1e-3)
     assert roof["traffic_frac"] == pytest.approx(2.2e9 / 650e-6 / 8e12, abs=1e-4)
     assert roof["valu"]["valu_busy"] == 0.88 and "profiles_note" not in roof

@@ -17,6 +17,7 @@
 #   tool:<script>[:args]:<tag>  python tools/<script> [args], output to <dir>/<tag>.out
 #   bin:<path>         a prebuilt probe binary (tools/gpu/<name>), output to <dir>/<name>.out
 #   kt:<script>[:args] the same under rocprofv3 --kernel-trace --stats (stats csv copied to <dir>)
+#   pmcbin:<binary>:<c1+c2..>[:<c1+..>]  rocprofv3 --pmc passes over a prebuilt probe (csv to <dir>)
 set -o pipefail
 O="gpurun_out/$1"
 shift
@@ -97,6 +98,22 @@ for step in "$@"; do
     bin:*)
       b=${step#bin:}
       timeout -k 10 120 "./$b" > "$O/$(basename "$b").out" 2>&1 || exit 1
+      ;;
+    pmcbin:*)
+      # pmcbin:<binary>:<pass>[:<pass>..], each pass '+'-separated counters: one rocprofv3 --pmc run of
+      # the prebuilt probe per pass (kernel-trace only beside the counters), csv into <dir>
+      IFS=: read -r _ b passes <<< "$step"
+      IFS=: read -ra plist <<< "$passes"
+      k=0
+      for pc in "${plist[@]}"; do
+        k=$((k+1))
+        cd /tmp && export TMPDIR=/tmp
+        timeout -s KILL 120 rocprofv3 --pmc ${pc//+/ } --kernel-trace --output-format csv -d /tmp/pmcbin_$k -o p -- \
+          "$R/$b" > "$R/$O/$(basename "$b")_pass$k.out" 2>&1 || exit 1
+        f=$(find /tmp/pmcbin_$k -name "*counter_collection.csv" | head -1)
+        [ -n "$f" ] && cp "$f" "$R/$O/$(basename "$b")_pass$k.csv"
+        cd "$R"
+      done
       ;;
     kt:*)
       IFS=: read -r _ script args <<< "$step"

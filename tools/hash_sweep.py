@@ -1,20 +1,42 @@
 #!/usr/bin/env python3
-"""Voxel-hash load-factor sweep (BASELINE config[2]) on the fused launch: a
-power-of-two device table of 2^17 slots filled to load factors 0.1 .. 0.95 by the blocks of more
-and more frames (the bench ring first, then other camera rings), the resize policy lifted to 0.97
-(TSDF_HASH_MAX_LOAD) so the table keeps its size; at each load the steady pass re-integrates the
-same 64 bench frames (lookups only): frames/s, Mvoxel-updates/s, mean / max probe distance,
-displaced keys.  Then the reference's own policy (resize at 0.75, hash_fusion.py:156-161,414-437)
-active on a 2^17 table through the whole run, so that double_table_size happens mid-run.  Also
-the 1024^3 @ 1 cm extent's cull cost (same frames, 2^22 buckets, 8x the bricks the cull walks).
-Prints one JSON object.
+"""Voxel-hash load-factor sweep on the shipped fused hash path (BASELINE config[2] "same 1000
+frames, 8^3 blocks, 2^22 buckets, load-factor sweep"; SURVEY §8(d) C3: loads 0.1 .. 0.9, probe
+mean / max and Mvox-upd/s at each point).
 
-  python tools/hash_sweep.py [--frames 400]
+The path priced is the reference's insert-with-linear-probing under its resize policy
+(hash_fusion.py:156-161 needs_resize, :166 get_load_factor, :199-276 add_hash_entry,
+:414-437 double_table_size), as the fused launch runs it: the cull of launch k finds or inserts
+the blocks of batch k+1 (csrc/tsdf_device.h cull_find_or_insert), the integrate of launch k+1
+updates them, and the call's end frees the blocks no frame updated (k_free_unused, tombstones).
+
+Each point is the bench's own hash leg -- the bench-ring frames, W warm-up batches, then the
+K-batch timed window (frames W*32 .. (W+K)*32-1), which inserts ~70k new blocks -- on a FRESH
+table of S slots, with the table's load placed by S and by filler blocks:
+
+  * S = 2^23, 2^22 (the bench's table), 2^21, 2^20 and 2^19 slots ("vary slots at fixed frames");
+  * where the frames' own blocks leave the table below the target load, filler blocks are
+    imported first (tsdf_hash_import_blocks).  They lie in brick layers above the room's ceiling
+    (the extent is extended in z; nothing there is ever updated: it is behind the ceiling by
+    more than the truncation), so they occupy slots exactly like live keys and cost the
+    integrate nothing -- only their probe cost remains, which is what is being measured;
+  * every point uses the same extended extent, and the dense grid is timed over the same extent
+    and window, so the cull's extra superbricks are in both (hash / dense ratio on equal work).
+
+At each point: the inserting window (the fresh table's first pass over the window: every new
+block of the window is inserted by a cull) and the repeat window (the same frames again: lookups,
+plus the few kept-but-unupdated bricks that are inserted and freed again).  Per window: kernel
+time per launch (HIP events), frames/s and Mvox-upd/s on kernel time and on wall time, cull
+lookups' mean / max probe distance, blocks inserted, tombstones left, bricks skipped.  The table
+is kept at its size through the window (TSDF_HASH_MAX_LOAD = 0.97, the 0.75 policy lifted: the
+load must reach 0.9); calls are synchronous per batch so that no growth headroom for launches in
+flight doubles a full table before it is measured (the asynchronous bench window is timed beside
+it at 2^22 slots for the difference).
+
+  python tools/hash_sweep.py [--steps 20] [--warmup 5] [--reps 2] > profiles/rNN_hash_sweep.json
 """
 import argparse
 import contextlib
 import json
-import math
 import os
 import sys
 import time
@@ -24,15 +46,27 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "union-thesis-slam_amd"))
 
+ROOM = 10.24
+VS = 0.02
+FILL_Z0 = 66  # first filler brick layer: voxels >= 528 (10.56 m), past the ceiling + truncation
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=400)
-    ap.add_argument("--loads", default="0.5,0.6,0.7,0.75,0.8,0.85,0.9,0.95")
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=2, help="fresh-table repeats per point (the fastest is kept)")
+    ap.add_argument("--loads", default="0.3,0.4,0.5,0.6,0.7,0.75,0.8,0.85,0.9",
+                    help="target loads at the end of the inserting window on 2^19 slots")
     a = ap.parse_args()
-    os.environ["TSDF_HASH_MAX_LOAD"] = "0.97"  # (read by tsdf_hash_create: per table)
+    os.environ["TSDF_HASH_MAX_LOAD"] = "0.97"  # (read by tsdf_hash_create)
     import torch
-    from tsdf_amd import hash_fusion, scene
+    from tsdf_amd import _ffi, grid_fusion, hash_fusion, scene
     dev = torch.device("cuda", 0)
     F = a.frames
     poses = scene.trajectory(F, seed=0, radius_frac=scene.BENCH_RING)
@@ -45,174 +79,159 @@ def main():
         rgb[s:s + len(c)] = c
     Tinv = np.ascontiguousarray(np.linalg.inv(poses))
     K = scene.intrinsics()
+    torch.cuda.synchronize()
+    dstride, cstride = 480 * 640 * 2, 480 * 640 * 3
 
-    def run(ht, sync=False):
-        ht.stats(reset=True)
+    def frames(vol, f0, n, sync, profile=False):
+        vol.set_profiling(profile)
+        vol.stats(reset=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv, hw=(480, 640), device_ptrs=True, sync=sync)
-        ht.sync()
-        dt = time.perf_counter() - t0
-        st = ht.stats()
-        if st["bricks_skipped"] and not sync:
-            raise RuntimeError("bricks skipped")
-        return dt, st
+        vol.integrate_batch(depth.data_ptr() + f0 * dstride, rgb.data_ptr() + f0 * cstride, K, Tinv[f0:f0 + n],
+                            hw=(480, 640), device_ptrs=True, sync=sync)
+        vol.sync()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, vol.stats()
 
-    def table(vs, cap, max_blocks):
+    def bounds(zb):
+        return np.array([[0.0, ROOM], [0.0, ROOM], [0.0, zb * 8 * VS - 0.5 * VS]])  # (ceil: zb*8 voxels)
+
+    def table(zb, S, max_blocks):
         with contextlib.redirect_stdout(sys.stderr):
-            return hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), vs, cap, max_blocks=max_blocks)
+            return hash_fusion.HashTable(bounds(zb), VS, S, max_blocks=max_blocks)
 
-    # Load factor on the fused launch: a power-of-two device table of S = 2^17 slots (every table
-    # the library builds is one) filled to each target load by the blocks of more and more frames
-    # (the bench ring, then other camera rings: up to 192k blocks, so every load up to 0.95 is
-    # reachable), the resize policy lifted; then the steady pass re-integrates the same 64 bench
-    # frames (their blocks exist: lookups only).
-    S = 1 << 17
-    rings = [scene.BENCH_RING, 0.30, 0.20, 0.36, 0.25, 0.12]
-    probe_n = 64
+    def grid(zb):
+        with contextlib.redirect_stdout(sys.stderr):
+            return grid_fusion.TSDFVolume(bounds(zb), VS)
 
-    def ring_frames(rf, n=1000):
-        ps = scene.trajectory(n, seed=0, radius_frac=rf)
-        sp = scene.make_spheres(0, ring_frac=scene.BENCH_RING)
-        dd = torch.empty((n, 480, 640), dtype=torch.int16, device=dev)
-        cc = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
-        for s0 in range(0, n, 50):
-            d, c = scene.render(ps[s0:s0 + 50], sp, seed=0, start=s0, device=dev, depth_dtype=torch.int16)
-            dd[s0:s0 + len(d)] = d
-            cc[s0:s0 + len(c)] = c
-        return dd, cc, np.ascontiguousarray(np.linalg.inv(ps))
+    B = 32
+    Wf, Kf = a.warmup * B, a.steps * B
 
-    ring_data = [(depth, rgb, Tinv)] + [None] * (len(rings) - 1)
+    def window_summary(dt, st, info, S):
+        L = max(1, st["kernel_launches"])
+        ks = st["kernel_ms"] / 1e3
+        return {"kernel_avg_us": round(1e6 * ks / L, 2), "launches": st["kernel_launches"],
+                "frames_per_s_kernel": round(Kf / ks, 1) if ks else None,
+                "frames_per_s_wall": round(Kf / dt, 1),
+                "mvox_updates_per_s_kernel": round(st["voxel_updates"] / ks / 1e6, 1) if ks else None,
+                "mean_probe": round(st["probe_steps"] / max(1, st["lookups"]), 4),
+                "max_probe": int(st["probe_max"]), "lookups": int(st["lookups"]),
+                "blocks_inserted": int(st["blocks_allocated"]), "bricks_skipped": int(st["bricks_skipped"]),
+                "live_after": int(info["used"]), "load_after": round(info["used"] / S, 4),
+                "tombstones_after": int(info["tombstones"]), "slots_after": int(info["slots"])}
 
-    def chunk(ht, r, f0, n, sync=True):
-        if ring_data[r] is None:
-            ring_data[r] = ring_frames(rings[r])
-        dd, cc, T = ring_data[r]
-        n = min(n, dd.shape[0] - f0)
-        if n <= 0:
-            return 0
-        ht.integrate_batch(dd[f0].data_ptr(), cc[f0].data_ptr(), K, T[f0:f0 + n], hw=(480, 640),
-                           device_ptrs=True, sync=sync)
-        return n
+    # ---- clock warm-up (bench.py --preheat-ms): integrate launches for ~300 ms -----------------
+    g = grid(64)
+    t_end = time.perf_counter() + 0.3
+    f0 = 0
+    while time.perf_counter() < t_end:
+        frames(g, f0 % (F - 20 * B), 20 * B, sync=False)
+        f0 += 20 * B
+    g.close()
+    del g
+    torch.cuda.empty_cache()
 
+    # ---- calibration: the window's own blocks (2^22 slots, no filler) -------------------------
+    zb0 = FILL_Z0
+    ht = table(zb0, 1 << 22, 1 << 18)
+    frames(ht, 0, Wf, sync=True)
+    live_start = int(ht.info()["used"])
+    frames(ht, Wf, Kf, sync=True)
+    live_end = int(ht.info()["used"])
+    ht.close()
+    del ht
+    log(f"calibration: live blocks {live_start} after the warm-up, {live_end} after the window")
+    S19 = 1 << 19
+    targets = [float(x) for x in a.loads.split(",")]
+    points = [(1 << 23, None), (1 << 22, None), (1 << 21, 0.1), (1 << 20, 0.2)] + [(S19, t) for t in targets]
+    max_fill = max(0 if t is None else max(0, int(round(t * S - live_end))) for S, t in points)
+    layers = (max_fill + 4095) // 4096
+    zb = FILL_Z0 + layers
+    log(f"extent: 512 x 512 x {8 * zb} voxels ({layers} filler layers, up to {max_fill} filler blocks)")
+    nb_extent = 64 * 64 * zb
+
+    # ---- dense grid over the same extent and window (the ratio's denominator) -----------------
+    dense = {}
+    for mode, sync in (("async", False), ("sync", True)):
+        best = None
+        for _ in range(a.reps):
+            g = grid(zb)
+            frames(g, 0, Wf, sync=False)
+            dt, st = frames(g, Wf, Kf, sync=sync, profile=True)
+            r = {"kernel_avg_us": round(1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), 2),
+                 "frames_per_s_wall": round(Kf / dt, 1), "launches": st["kernel_launches"],
+                 "voxel_updates": int(st["voxel_updates"])}
+            if best is None or r["kernel_avg_us"] < best["kernel_avg_us"]:
+                best = r
+            g.close()
+            del g
+            torch.cuda.empty_cache()
+        dense[mode] = best
+        log(f"dense {mode}: {best}")
+    d_us = dense["async"]["kernel_avg_us"]
+
+    # ---- the bench's own configuration (2^22 slots, asynchronous window) ----------------------
+    bench_like = None
+    for _ in range(a.reps):
+        ht = table(zb, 1 << 22, 1 << 15)
+        frames(ht, 0, Wf, sync=True)
+        dt, st = frames(ht, Wf, Kf, sync=False, profile=True)
+        r = window_summary(dt, st, ht.info(), 1 << 22)
+        if bench_like is None or r["kernel_avg_us"] < bench_like["kernel_avg_us"]:
+            bench_like = r
+        ht.close()
+        del ht
+        torch.cuda.empty_cache()
+    bench_like["over_dense"] = round(bench_like["kernel_avg_us"] / d_us, 3)
+    log(f"bench-like async 2^22: {bench_like}")
+
+    # ---- the sweep ----------------------------------------------------------------------------
     out = []
-    for lf in [float(x) for x in a.loads.split(",")]:
-        ht = table(0.02, S, 64 ** 3)
-        chunk(ht, 0, 0, probe_n)
-        r, f = 0, probe_n
-        while ht.info()["used"] < lf * S and r < len(rings):
-            n = chunk(ht, r, f, 8)  # (8 frames at a time: the load lands near its target)
-            f += n
-            if n == 0 or f >= 1000:
-                r, f = r + 1, 0
-        info = ht.info()
-        res = {"target_load": lf, "slots": int(info["slots"]), "blocks_live": int(info["used"]),
-               "load_factor": round(info["used"] / info["slots"], 4), "displaced": int(info["displaced"]),
-               "max_probe_in_table": int(info["max_probe"])}
-        # (synchronous calls of one launch's frames: an asynchronous call keeps two launches'
-        # lists of headroom in the slots, and would double a table this full before it starts)
-        ht.set_profiling(True)
-        ht.stats(reset=True)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        reps, nb = 4, ht.frames_per_launch()
-        for _ in range(reps):
-            for f0 in range(0, probe_n, nb):
-                chunk(ht, 0, f0, nb, sync=True)
-        ht.sync()
-        dt = time.perf_counter() - t0
-        st = ht.stats()
-        if st["bricks_skipped"] or ht.info()["slots"] != res["slots"]:
-            raise RuntimeError("bricks skipped or table resized in the steady pass")
-        if res["slots"] != S:  # the fill passed TSDF_HASH_MAX_LOAD: the table doubled before the pass
-            res["note"] = "the fill passed 0.97 of 2^17 slots and the table doubled; measured at the load shown"
-        res["steady_pass"] = {"frames_per_s": round(reps * probe_n / dt, 1),
-                              "kernel_avg_us": round(1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), 1),
-                              "frames_per_launch": nb,
-                              "mvox_updates_per_s": round(st["voxel_updates"] / dt / 1e6, 1),
-                              "mean_probe": round(st["probe_steps"] / max(1, st["lookups"]), 3),
-                              "max_probe": int(st["probe_max"])}
-        print(json.dumps(res), file=sys.stderr, flush=True)
-        out.append(res)
-        del ht
-        torch.cuda.empty_cache()
-    # The reference's policy active: a 2^17 table, TSDF_HASH_MAX_LOAD unset (0.75), the bench's 1000
-    # frames asynchronously and then synchronously per batch of 8 (the drop-in's checks): the table
-    # doubles when live keys reach 0.75 of it, mid-run, as double_table_size does
-    os.environ.pop("TSDF_HASH_MAX_LOAD", None)
-    policy = {}
-    for mode in ("async", "sync_per_batch"):
-        ht = table(0.02, S, 1 << 15)
-        caps = [int(ht.info()["capacity"])]
-        ht.stats(reset=True)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        skipped0 = 0
-        if mode == "async":
-            # a fresh table's first batch runs synchronously (as the library does it for an
-            # asynchronous first call): its pool overflow re-runs exactly, and bricks_skipped
-            # counts those re-run bricks; an asynchronous skip raises TSDF_E_CAPACITY at sync
-            nb = ht.frames_per_launch()
-            ht.integrate_batch(depth.data_ptr(), rgb.data_ptr(), K, Tinv[:nb], hw=(480, 640), device_ptrs=True)
-            skipped0 = ht.stats()["bricks_skipped"]
-            ht.integrate_batch(depth[nb:].data_ptr(), rgb[nb:].data_ptr(), K, Tinv[nb:], hw=(480, 640),
-                               device_ptrs=True, sync=False)
-        else:
-            for f0 in range(0, F, 8):
-                ht.integrate_batch(depth[f0].data_ptr(), rgb[f0].data_ptr(), K, Tinv[f0:f0 + 8], hw=(480, 640),
-                                   device_ptrs=True, sync=True)
-                c = int(ht.info()["capacity"]) if f0 % 64 == 0 else caps[-1]
-                if c != caps[-1]:
-                    caps.append(c)
-        ht.sync()
-        dt = time.perf_counter() - t0
-        st = ht.stats()
-        info = ht.info()
-        if st["bricks_skipped"] != skipped0 and mode == "async":
-            raise RuntimeError("bricks skipped")
-        if info["capacity"] != caps[-1]:
-            caps.append(int(info["capacity"]))
-        policy[mode] = {"frames_per_s": round(F / dt, 1), "table_size_start": S, "table_size_end": int(info["capacity"]),
-                        "table_sizes_seen": caps, "doublings": int(round(math.log2(info["capacity"] / S))),
-                        "blocks_live": int(info["used"]), "load_factor_end": round(info["used"] / info["capacity"], 4),
-                        "mean_probe": round(st["probe_steps"] / max(1, st["lookups"]), 3),
-                        "max_probe": int(st["probe_max"])}
-        print(json.dumps({"policy": policy}), file=sys.stderr, flush=True)
-        del ht
-        torch.cuda.empty_cache()
-    os.environ["TSDF_HASH_MAX_LOAD"] = "0.97"
-    # the reference's own table sizes (HashTable(map_size=1000000), hash_fusion.py:34; 2000000 in
-    # hash_demo1.py:110) against 2^22: the device table takes the next power of two of slots, so
-    # every size runs the fused launch; steady pass over the same frames after an allocating pass
-    sizes = {}
-    for ms in (1000000, 2000000, 1 << 22):
-        ht = table(0.02, ms, 1 << 15)
-        run(ht, sync=True)  # allocate (a fresh pool's growth, overflow re-runs exact)
-        best = min(run(ht)[0] for _ in range(3))
-        info = ht.info()
-        sizes[str(ms)] = {"frames_per_s": round(F / best, 1), "device_slots": int(info["slots"]),
-                          "table_size": int(ht._table_size), "blocks_live": int(info["used"])}
-        print(json.dumps({"reference_sizes": sizes}), file=sys.stderr, flush=True)
-        del ht
-        torch.cuda.empty_cache()
-    # 1024^3 @ 1 cm extent (config[4]'s): the cull walks 2^21 bricks per batch
-    ext = {}
-    for vs, nb in ((0.02, 64 ** 3), (0.01, 128 ** 3)):
-        ht = table(vs, 1 << 22, min(nb, 1 << 20))
-        run(ht)  # allocate
-        ht.set_profiling(True)
-        dt, st = run(ht)
-        ext[f"{int(round(10.24 / vs))}^3"] = {
-            "frames_per_s": round(F / dt, 1), "kernel_avg_us": round(1e3 * st["kernel_ms"] / max(1, st["kernel_launches"]), 1),
-            "bricks_in_extent": nb, "bricks_visited_per_frame": round(st["bricks_visited"] / F),
-            "voxel_updates_per_frame": round(st["voxel_updates"] / F), "blocks_live": int(ht.info()["used"])}
-        print(json.dumps(ext), file=sys.stderr, flush=True)
-        del ht
-        torch.cuda.empty_cache()
-    print(json.dumps({"sweep": out, "frames": F, "slots": S, "policy_0_75": policy, "extent_cost": ext,
-                      "reference_sizes": sizes,
-                      "volume": "512^3 @ 2 cm extent, 8^3 blocks; steady pass = the first 64 bench-ring frames x 4",
-                      "kernel": "k_fused_hash<0> (power-of-two device table, z-half waves)"}))
+    for S, target in points:
+        fill = 0 if target is None else max(0, int(round(target * S - live_end)))
+        i = np.arange(fill)
+        fill_xyz = np.stack([i % 64, (i // 64) % 64, FILL_Z0 + i // 4096], axis=1).astype(np.int32)
+        best = None
+        for _ in range(a.reps):
+            ht = table(zb, S, min(nb_extent, fill + live_end + (1 << 16)))
+            if fill:
+                ht.import_blocks(fill_xyz, None, None, None)
+            frames(ht, 0, Wf, sync=True)
+            i0 = ht.info()
+            dt, st = frames(ht, Wf, Kf, sync=True, profile=True)
+            ins = window_summary(dt, st, ht.info(), S)
+            dt2, st2 = frames(ht, Wf, Kf, sync=True, profile=True)
+            rep = window_summary(dt2, st2, ht.info(), S)
+            r = {"slots": S, "target_load": target, "filler_blocks": fill,
+                 "load_window_start": round(i0["used"] / S, 4), "load_window_end": ins["load_after"],
+                 "inserting": ins, "repeat": rep}
+            if best is None or ins["kernel_avg_us"] < best["inserting"]["kernel_avg_us"]:
+                best = r
+            ht.close()
+            del ht
+            torch.cuda.empty_cache()
+        best["inserting"]["over_dense"] = round(best["inserting"]["kernel_avg_us"] / d_us, 3)
+        best["repeat"]["over_dense"] = round(best["repeat"]["kernel_avg_us"] / d_us, 3)
+        log(json.dumps(best))
+        out.append(best)
+    base = next(p for p in out if p["target_load"] == 0.1)["inserting"]["kernel_avg_us"]
+    for p in out:
+        p["inserting"]["over_load_0_1"] = round(p["inserting"]["kernel_avg_us"] / base, 3)
+    print(json.dumps({
+        "build_id": _ffi.build_id(),
+        "workload": ("config[2]: bench-ring frames %d..%d (the bench's timed window after %d warm-up frames) into a voxel "
+                     "hash over 512x512x%d @ 2 cm (the 512^3 room + %d filler brick layers above its ceiling), 8^3 blocks"
+                     % (Wf, Wf + Kf - 1, Wf, 8 * zb, layers)),
+        "frames_per_launch": B, "window_frames": Kf,
+        "calibration": {"live_after_warmup": live_start, "live_after_window": live_end},
+        "dense_same_extent": dense, "bench_like_async_2_22": bench_like,
+        "sweep": out,
+        "notes": ("load = live block keys / slots; filler blocks (imported, never updated) place the load; "
+                  "calls synchronous per batch, TSDF_HASH_MAX_LOAD 0.97 so no point doubles its table; "
+                  "kernel time from HIP events on the handle's stream; over_dense = inserting (or repeat) "
+                  "launch / the dense launch over the same extent and window (asynchronous); fastest of "
+                  "%d fresh-table repeats per point" % a.reps),
+        "reference": "hash_fusion.py:156-161,166,199-276,414-437"}))
 
 
 if __name__ == "__main__":

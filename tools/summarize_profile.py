@@ -18,10 +18,14 @@ whose first two launches fill the pipeline); the bench line records the dispatch
 the first timed integrate launch (roofline.first_timed_launch_index), and the K launches from it
 are the timed ones.
 
-FETCH_SIZE/WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
-coalesced read (MI355X_MICROARCH.md, HBM section); the integrate kernel's HBM reads are its
-16-B/lane brick-state loads (the per-frame depth/colour gathers are L2/MALL-resident), so the
-read side is doubled.  WRITE_SIZE is exact for 16-B/lane stores.
+FETCH_SIZE/WRITE_SIZE are KiB.  FETCH_SIZE on gfx950 is (TCC_BUBBLE*128 + (RDREQ - BUBBLE - RDREQ_32B)*64
++ RDREQ_32B*32) (rocprofiler-sdk counter_defs.yaml): a 128-B memory-side read request is tallied at 64 B,
+which is the guide's "half of a wide streaming read" -- and the gathers fill L2 lines by requests of
+their own sizes, so no single factor fits a kernel that does both.  The RDREQ pass counts the L2's
+memory-side read requests by size (TCC_EA0_RDREQ_32B / _64B / _128B); the read bytes are
+32*n32 + 64*n64 + 128*n128, checked against known byte counts by tools/gpu/fetch_probe.hip
+(profiles/r06_fetch_probe/).  WRITE_SIZE is exact for 16-B/lane stores.  Both count L2 memory-side
+traffic: Infinity-Cache hits included, so an upper bound on DRAM bytes.
 """
 import csv
 import json
@@ -80,6 +84,28 @@ def pmc_timed(path, counter, first, ids=None):
     return [v for _, v in t]
 
 
+RDREQ = ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum"]
+
+
+def counter_rows(path, kernel):
+    """{dispatch: {counter: value summed over dimensions}} of one kernel in a pmc csv."""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if kernel not in r["Kernel_Name"]:
+            continue
+        d = per.setdefault(int(r["Dispatch_Id"]), {})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return per
+
+
+def request_bytes(m):
+    """Read bytes from the request counts by size, and the requests the sizes do not cover."""
+    n32, n64, n128 = (m.get(c, 0.0) for c in RDREQ[1:])
+    return {"rdreq": m.get(RDREQ[0]), "rdreq_32b": n32, "rdreq_64b": n64, "rdreq_128b": n128,
+            "read_bytes_by_request_size": 32 * n32 + 64 * n64 + 128 * n128,
+            "requests_unsized": (m.get(RDREQ[0]) or 0.0) - n32 - n64 - n128}
+
+
 def main(tag):
     src = os.path.join(REPO, "gpurun_out", "profile")
     dst = os.path.join(REPO, "profiles")
@@ -105,17 +131,27 @@ def main(tag):
     pw = bench_line(os.path.join(src, "pmc_WRITE_SIZE.json"))
     fetch = pmc_timed(os.path.join(src, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", first_index(pl))
     write = pmc_timed(os.path.join(src, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", first_index(pw))
+    pr = bench_line(os.path.join(src, "pmc_RDREQ.json"))
+    per = counter_rows(os.path.join(src, "pmc_RDREQ.csv"), KERNEL)
+    ids = [d for d, _ in timed([(d, m.get(RDREQ[0], 0.0)) for d, m in per.items()], first_index(pr))]
+    reqs = [request_bytes(per[d]) for d in ids]
     sys.path.insert(0, REPO)
     import bench
     fk = statistics.median(fetch) * 1024.0
     wk = statistics.median(write) * 1024.0
+    rb = statistics.median(r["read_bytes_by_request_size"] for r in reqs)
     summary = {"kernel": KERNEL, "build_id": pl.get("build_id"), "workload": bench.WORKLOAD,
                "window": f"bench.py --gpus 1 --steps {K} --warmup {W}: the {K} timed launches (median)",
-               "launches_sampled": [len(fetch), len(write)],
-               "fetch_bytes_raw": fk, "fetch_bytes_corrected": 2 * fk, "write_bytes": wk,
-               "hbm_bytes_per_launch": round(2 * fk + wk),
+               "launches_sampled": [len(fetch), len(write), len(reqs)],
+               "fetch_size_bytes_raw": fk, "write_bytes": wk,
+               "read_requests_median": {k: statistics.median(r[k] for r in reqs) for k in reqs[0]},
+               "read_bytes": rb,
+               "l2_memside_bytes_per_launch": round(rb + wk),
+               "raw_bytes_per_launch": round(fk + wk),
                "timed_launch_avg_us_under_rocprof": round(statistics.mean(durs), 2),
-               "note": __doc__.strip().splitlines()[-4:]}
+               "build_ids": {"FETCH_SIZE": pl.get("build_id"), "WRITE_SIZE": pw.get("build_id"),
+                             "RDREQ": pr.get("build_id")},
+               "note": " ".join(l.strip() for l in __doc__.strip().splitlines()[-8:])}
     with open(os.path.join(dst, f"pmc_integrate_{tag}.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
@@ -185,23 +221,28 @@ def hash_profile(tag):
     blocks = {"inserting": {}, "no_alloc_repeat": {}}
     for path, names in ((os.path.join(src, "pmc_FETCH_SIZE.csv"), ["FETCH_SIZE"]),
                         (os.path.join(src, "pmc_WRITE_SIZE.csv"), ["WRITE_SIZE"]),
+                        (os.path.join(src, "pmc_RDREQ.csv"), RDREQ),
                         (os.path.join(REPO, "gpurun_out", "pmc_sq", "pmc_sq.csv"), SQ_NAMES)):
         ins, rep = hash_windows(path)
         for key, rows in (("inserting", ins), ("no_alloc_repeat", rep)):
             for n in names:
                 blocks[key][n] = statistics.median(r[n] for r in rows)
     for key, m in blocks.items():
-        m["hbm_bytes"] = round(1024 * (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]))
+        m.update(request_bytes(m))
+        m["raw_bytes"] = round(1024 * (m["FETCH_SIZE"] + m["WRITE_SIZE"]))
+        m["l2_memside_bytes"] = round(m["read_bytes_by_request_size"] + 1024 * m["WRITE_SIZE"])
         m["valu_busy_per_simd"] = round(m["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * m["GRBM_GUI_ACTIVE"] / 8), 3)
         m["wait_any_frac"] = round(m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"], 3)
     ins = blocks["inserting"]
     out["build_id"] = bench_line(os.path.join(src, "pmc_FETCH_SIZE.json")).get("build_id")
-    out["hbm_bytes_per_launch"] = ins["hbm_bytes"]
+    out["l2_memside_bytes_per_launch"] = ins["l2_memside_bytes"]
+    out["raw_bytes_per_launch"] = ins["raw_bytes"]
     out["median_per_launch"] = {n: ins[n] for n in SQ_NAMES}
     out["valu_busy_per_simd"] = ins["valu_busy_per_simd"]
     out["wait_any_frac"] = ins["wait_any_frac"]
     out["no_alloc_repeat"] = blocks["no_alloc_repeat"]
-    out["note"] = ("FETCH_SIZE doubled per the gfx950 rule (as pmc_integrate_*); SQ cycle counters in quad-cycles; "
+    out["note"] = ("read bytes from the L2's memory-side read requests by size (32/64/128 B, as pmc_integrate_*; "
+                   "FETCH_SIZE tallies a 128-B request at 64 B); SQ cycle counters in quad-cycles; "
                    "busy = ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")
     with open(os.path.join(REPO, "profiles", f"pmc_hash_{tag}.json"), "w") as f:
         json.dump(out, f, indent=1)

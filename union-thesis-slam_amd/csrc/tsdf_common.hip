@@ -325,17 +325,19 @@ class CopyPool {
     }
     bool depth_mm(unsigned short* dst, const double* src, size_t n) {  // depth_mm_any over the pool
         if (workers_.empty() || n < (32u << 10)) return depth_mm_any(dst, src, n);
-        bad_ = 0;
-        run_job(1, dst, src, n, 64);
-        return bad_ == 0;
+        return run_job(1, dst, src, n, 64);
     }
 
   private:
     // job 0: copy `n` bytes; job 1: convert `n` depth values; shares of `chunk` units (a multiple
-    // of `align`), share 0 on the calling thread
-    void run_job(int job, void* dst, const void* src, size_t n, size_t align) {
+    // of `align`), share 0 on the calling thread.  Returns false when a share of a conversion
+    // found a value that is not exact millimetres: the flag belongs to the job -- cleared and read
+    // under call_, so a concurrent caller (handles driven from several threads: ctypes releases
+    // the GIL) can neither clear another job's flag nor see it (round-5 advisor finding)
+    bool run_job(int job, void* dst, const void* src, size_t n, size_t align) {
         const int nw = (int)workers_.size();
         std::lock_guard<std::mutex> call(call_);  // one job at a time through the pool
+        bad_ = 0;
         const size_t parts = (size_t)nw + 1;
         const size_t chunk = ((n + parts - 1) / parts + align - 1) / align * align;
         {
@@ -352,6 +354,7 @@ class CopyPool {
         share(job, (char*)dst, (const char*)src, n, chunk, 0);
         std::unique_lock<std::mutex> g(m_);
         done_.wait(g, [&] { return left_ == 0; });
+        return bad_ == 0;  // (every share has finished: the workers' flags are in)
     }
     void share(int job, char* d, const char* s, size_t n, size_t chunk, int k) {
         const size_t o = (size_t)k * chunk;
@@ -576,14 +579,17 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
     // quarter of the bytes into the bounce slot and over PCIe, the same metres in the kernels
     // (depth_mm_any); a batch holds one kind, so a frame that does not convert after u16 ones
     // sends the caller back to flush them first (kDeferFlush), and then starts an f64 batch
+    // (after such a frame the next kMmBackoff batches go as f64 without trying: mm_backoff)
     bool staged = false;
-    if (dk == TSDF_DEPTH_F64_M && defer_mm && (i == 0 || dfr.dk == TSDF_DEPTH_U16_MM)) {
+    const bool try_mm = i == 0 ? mm_backoff == 0 : dfr.dk == TSDF_DEPTH_U16_MM;
+    if (i == 0 && mm_backoff > 0) --mm_backoff;
+    if (dk == TSDF_DEPTH_F64_M && defer_mm && try_mm) {
         if (CopyPool::get().depth_mm((unsigned short*)hst_depth[dfr.slot] + npx * i, (const double*)depth, npx)) {
             dfr.dk = TSDF_DEPTH_U16_MM;
             staged = true;
-        } else if (i > 0) {
-            return kDeferFlush;
         } else {
+            mm_backoff = kMmBackoff;
+            if (i > 0) return kDeferFlush;
             dfr.dk = TSDF_DEPTH_F64_M;
         }
     }

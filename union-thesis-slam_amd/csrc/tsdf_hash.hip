@@ -194,6 +194,11 @@ struct tsdf_hash {
     }
     long long tomb_est = 0;       // PoolState::tombs at the last read or pool report (remove() and
                                   // k_free_unused add tombstones)
+    // allocating launches issued before the table's last rebuild (resize_table drains the stream, so
+    // every launch < rehash_seq had finished): their pool reports carry the tombstone count of the
+    // table that was replaced and must not be read back into tomb_est (table_tombs)
+    long long rehash_seq = 0;
+    long long table_rebuilds = 0;  // rebuilds at the same size (tombstone purges), for the tests
     bool async_pending = false;   // asynchronous launches since the last overflow check
     // table load factor that triggers a doubling: the reference's hard-coded 0.75 (hash_fusion.py:
     // 156-161); TSDF_HASH_MAX_LOAD overrides it for the load-factor sweep (tools/hash_sweep.py)
@@ -745,6 +750,8 @@ int resize_table(tsdf_hash* h, long long new_cap) {
     TSDF_HIP(hipStreamSynchronize(B.stream));
     fresh.keep();
     h->tomb_est = 0;
+    h->host_st.tombs = 0;
+    h->rehash_seq = h->seq;
     (void)hipFree(h->t.keys);
     (void)hipFree(h->t.vals);
     h->t.keys = nt.keys;
@@ -759,10 +766,67 @@ long long next_pow2(long long n) {
     return p;
 }
 
-// The load-factor policy's doubling: the API size and the device slots together.
+// The overflow re-run's doubling (hash_after_batch: a brick found no slot): the API size and the
+// device slots together -- bounded like table_room's, so a table that stays full for another
+// reason fails with TSDF_E_CAPACITY instead of doubling until the device is out of memory.
 int grow_table(tsdf_hash* h) {
+    const long long bound = std::max<long long>(next_pow2(h->map_size),
+                                                next_pow2((long long)(2.0 * (double)h->b.n_bricks / h->max_load) + 64));
+    if (next_pow2(2 * h->map_size) > bound)
+        return set_error(TSDF_E_CAPACITY, "hash table: a table of %lld slots for %lld bricks is full; not doubling "
+                         "further", (long long)h->t.capacity, (long long)h->b.n_bricks);
     TSDF_TRY(resize_table(h, next_pow2(2 * h->map_size)));
     h->map_size *= 2;
+    return TSDF_OK;
+}
+
+// The tombstone count of a pool report of launch `seq`, or 0 when that launch ran on a table that
+// has since been rebuilt (rehash_seq): the rebuild cleared those tombstones.  Round 5 took the max
+// of the estimate and every report, so a report written just before a rebuild brought the old
+// count back and the policy below counted tombstones the table no longer had.
+long long table_tombs(const tsdf_hash* h, long long seq, long long report_tombs) {
+    return seq < h->rehash_seq ? h->tomb_est : std::max(h->tomb_est, report_tombs);
+}
+
+// Room in the table for `live` keys plus `extra` new ones, keeping the reference's policy
+// (needs_resize / double_table_size, hash_fusion.py:156-161,414-437): the table size doubles while
+// live + extra keys reach max_load of it -- it grows with its keys, as the reference's does, never
+// with deletions; tombstones (k_free_unused, remove) count against the slots but only make the
+// table rebuild at its size (a purge), so a long per-frame run whose calls free their unused
+// blocks does not double the table (round 5 doubled for them).  The doublings are computed first
+// and done as ONE rehash; `slots_room` > 0 also keeps live + extra + tombstones below 31/32 of
+// the device slots (asynchronous calls: room for the launches in flight, whatever the policy).
+// Live keys are bricks of the volume, so extra is clamped to the bricks not yet keyed and the
+// sizes asked are bounded by 2 * n_bricks / max_load; a count outside that is a wrong estimate
+// and fails with TSDF_E_CAPACITY instead of doubling until the device runs out of memory (round
+// 5's OOM).
+int table_room(tsdf_hash* h, long long live, long long extra, long long tombs, bool slots_room = false) {
+    const long long nb = h->b.n_bricks;
+    if (live < 0 || live > nb || tombs < 0 || tombs > h->t.capacity)
+        return set_error(TSDF_E_CAPACITY, "hash table: implausible counts (%lld live keys, %lld tombstones) for %lld "
+                         "bricks and %lld slots", live, tombs, nb, (long long)h->t.capacity);
+    extra = std::max<long long>(0, std::min<long long>(extra, nb - live));
+    const long long bound = std::max<long long>(h->map_size, (long long)(2.0 * (double)nb / h->max_load) + 64);
+    long long ms = h->map_size;
+    const auto slots_full = [&](long long m, long long t) {
+        const long long cap = next_pow2(m);
+        return slots_room && live + extra + t >= cap - cap / 32;
+    };
+    while ((double)(live + extra) >= h->max_load * (double)ms || slots_full(ms, 0)) {
+        ms *= 2;
+        if (ms > bound)
+            return set_error(TSDF_E_CAPACITY, "hash table: %lld live keys + %lld of room would need a table of more "
+                             "than %lld (max_load %.2f, %lld bricks)", live, extra, bound, h->max_load, nb);
+    }
+    if (ms != h->map_size) {  // one rehash to the policy's size (it drops the tombstones too)
+        TSDF_TRY(resize_table(h, next_pow2(ms)));
+        h->map_size = ms;
+        return TSDF_OK;
+    }
+    if ((double)(live + extra + tombs) >= h->max_load * (double)ms || slots_full(ms, tombs)) {
+        TSDF_TRY(resize_table(h, h->t.capacity));  // the purge: same size, no tombstones
+        ++h->table_rebuilds;
+    }
     return TSDF_OK;
 }
 
@@ -794,8 +858,7 @@ int ensure_room(tsdf_hash* h, bool fresh = false) {
     const long long step = h->recent_growth();
     if (h->vmm ? live + 2 * step > h->t.max_blocks : (double)(live + 64) >= 0.75 * (double)h->t.max_blocks)
         TSDF_TRY(grow_pool(h, pool_target(h, live + 3 * step)));
-    while ((double)(live + h->host_st.tombs) >= h->max_load * (double)h->map_size) TSDF_TRY(grow_table(h));
-    return TSDF_OK;
+    return table_room(h, live, 0, h->host_st.tombs);
 }
 
 // Bricks skipped by asynchronous launches: their batches' frames are gone, so they cannot be
@@ -855,19 +918,17 @@ int async_room(tsdf_hash* h, long long s) {
     if (!h->async_grow) return TSDF_OK;
     const long long used = r.pool_top - r.free_count;
     h->note_live(used);
-    h->tomb_est = std::max(h->tomb_est, r.tombs);
+    h->tomb_est = table_tombs(h, s - 2, r.tombs);
     // (the copy path keeps the pool's 1/12 as a floor of the estimate too, and doubles)
     const long long step = h->vmm ? h->recent_growth() : std::max<long long>(h->recent_growth(), h->t.max_blocks / 12);
     const long long need = used + std::max<long long>(3 * step, 2 * r.listed + step);
     if (need > h->t.max_blocks) TSDF_TRY(grow_pool(h, pool_target(h, need + step)));
-    while ((double)(used + 3 * h->recent_growth() + h->tomb_est) >= h->max_load * (double)h->map_size)
-        TSDF_TRY(grow_table(h));
+    TSDF_TRY(table_room(h, used, 3 * h->recent_growth(), h->tomb_est));
     // ... and the table's slots, whatever the load-factor policy allows (TSDF_HASH_MAX_LOAD up to
     // 0.99, or a jump in growth just below 0.75): the same two lists' worth of new keys must fit
     // below 31/32 of the slots, or launch s could find the table full and skip bricks
     const long long burst = std::max<long long>(3 * h->recent_growth(), 2 * r.listed + h->recent_growth());
-    while (used + h->tomb_est + burst >= h->t.capacity - h->t.capacity / 32) TSDF_TRY(grow_table(h));
-    return TSDF_OK;
+    return table_room(h, used, burst, h->tomb_est, true);
 }
 
 // One hash integrate pass over a batch: the listed bricks (list/count from k_cull, or an
@@ -1147,7 +1208,7 @@ int hash_settle(tsdf_hash* h) {
         h->host_st.free_count = r.free_count;
         h->host_st.n_overflow = 0;
         h->host_st.cursor = 0;
-        h->tomb_est = std::max(h->tomb_est, r.tombs);
+        h->tomb_est = table_tombs(h, h->pend.seq, r.tombs);
         h->host_st.tombs = h->tomb_est;
         return ensure_room(h, true);
     }
@@ -1202,10 +1263,7 @@ int insert_block_keys(tsdf_hash* h, const std::vector<unsigned long long>& keys,
     TSDF_TRY(read_state(h));
     InfoDev inf{};
     TSDF_TRY(info_raw(h, &inf));
-    while ((double)(inf.used + inf.tomb + nk) >= h->max_load * (double)h->map_size) {
-        TSDF_TRY(grow_table(h));
-        TSDF_TRY(info_raw(h, &inf));
-    }
+    TSDF_TRY(table_room(h, (long long)inf.used, nk, (long long)inf.tomb));
     if (h->host_st.pool_top + nk > h->t.max_blocks - h->host_st.free_count)
         TSDF_TRY(grow_pool(h, pool_target(h, h->host_st.pool_top + 2 * nk)));
     void* dkeys;

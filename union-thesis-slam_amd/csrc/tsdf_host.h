@@ -85,6 +85,11 @@ struct Base {
     // deferred f64-metre frames that are all RN(k / 1000) staged as u16 millimetres (defer_push;
     // TSDF_DEFER_MM=0: as they come)
     bool defer_mm = true;
+    // deferred batches still to be staged as f64 without trying u16 after a frame that was not
+    // exact millimetres: a stream that mixes the two kinds would otherwise flush a u16 batch at
+    // every such frame (batches of one or two frames; round-5 advisor finding)
+    int mm_backoff = 0;
+    static constexpr int kMmBackoff = 4;
     const char* call_color_end = nullptr;  // end of the current call's device colour array (begin_call)
     // Per-batch buffers of the CURRENT buffer set (use_set).
     float* pyr = nullptr;      // `batch` per-frame max-depth pyramids
