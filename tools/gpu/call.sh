@@ -18,6 +18,7 @@
 #   bin:<path>         a prebuilt probe binary (tools/gpu/<name>), output to <dir>/<name>.out
 #   kt:<script>[:args] the same under rocprofv3 --kernel-trace --stats (stats csv copied to <dir>)
 #   pmcbin:<binary>:<c1+c2..>[:<c1+..>]  rocprofv3 --pmc passes over a prebuilt probe (csv to <dir>)
+#   dropthreads:<t1+t2..>  per-frame drop-in rate per copy-pool size (tools/gpu/dropin_threads.sh)
 set -o pipefail
 O="gpurun_out/$1"
 shift
@@ -98,6 +99,11 @@ for step in "$@"; do
     bin:*)
       b=${step#bin:}
       timeout -k 10 120 "./$b" > "$O/$(basename "$b").out" 2>&1 || exit 1
+      ;;
+    dropthreads:*)
+      # dropthreads:<t1+t2+..>  the per-frame drop-in rate for each copy-pool size (dropin_threads.sh)
+      ts=${step#dropthreads:}
+      bash tools/gpu/dropin_threads.sh "$O/dropin_threads.jsonl" ${ts//+/ } 2> "$O/dropin_threads.err" || exit 1
       ;;
     pmcbin:*)
       # pmcbin:<binary>:<pass>[:<pass>..], each pass '+'-separated counters: one rocprofv3 --pmc run of
