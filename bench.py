@@ -55,6 +55,8 @@ SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r06.json")
 HASH_WORKLOAD = ("config[2]: the same frames into a voxel hash over the 512^3 @ 2 cm extent (8^3 blocks, 2^22 "
                  "slots, pool grown from 2^15 blocks)")
 HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r06.json")  # traffic + SQ of k_fused_hash<0, true>
+# config[2]'s load-factor sweep (tools/hash_sweep.py), quoted only for the library build it measured
+HASH_SWEEP = os.path.join(REPO, "profiles", "r06_hash_sweep.json")
 
 
 def log(*a):
@@ -172,6 +174,27 @@ def attach_profiles(roof, st, build_id, pmc_path, sq_path, workload):
                                   "HBM moves frac (algorithmic) / traffic_frac (measured) of its peak")
     if why:
         roof["profiles_note"] = "; ".join(why)
+
+
+def load_sweep(build_id, path=HASH_SWEEP):
+    """BASELINE config[2]'s load-factor sweep, summarised, when the committed sweep measured this
+    library build (else a note saying why it is absent)."""
+    rel = os.path.relpath(path, REPO)
+    if not os.path.exists(path):
+        return {"note": f"no {rel}"}
+    with open(path) as fh:
+        p = json.loads(fh.read().strip().splitlines()[-1])
+    if p.get("build_id") != build_id:
+        return {"note": f"{rel} measured library build {p.get('build_id')}, this is {build_id}"}
+    pts = [{"slots": q["slots"], "load_window_end": q["load_window_end"],
+            "inserting_kernel_us": q["inserting"]["kernel_avg_us"],
+            "inserting_over_dense": q["inserting"]["over_dense"],
+            "inserting_over_load_0_1": q["inserting"].get("over_load_0_1"),
+            "repeat_kernel_us": q["repeat"]["kernel_avg_us"],
+            "mean_probe": q["inserting"]["mean_probe"], "max_probe": q["inserting"]["max_probe"],
+            "tombstones_after": q["inserting"]["tombstones_after"]} for q in p["sweep"]]
+    return {"source": rel + " (tools/hash_sweep.py, build " + build_id + ")", "workload": p.get("workload"),
+            "dense_same_extent_kernel_us": p["dense_same_extent"]["async"]["kernel_avg_us"], "points": pts}
 
 
 def integrate_roofline(st, frames, kernel, first_timed=None, blocks_touched=None):
@@ -594,6 +617,7 @@ def main():
         if hroof is not None:
             attach_profiles(hroof, hs, _ffi.build_id(), HASH_PROFILE, HASH_PROFILE, HASH_WORKLOAD)
             hash_res["roofline"] = hroof
+        hash_res["load_sweep"] = load_sweep(_ffi.build_id())
         log(f"[rank {rank}] hash: {Kf / hdt:.0f} frames/s, load {hash_res['load_factor']}, "
             f"pool {info['pool_capacity']} blocks for {info['used']} live")
         ht.close()

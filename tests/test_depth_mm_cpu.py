@@ -50,3 +50,29 @@ def test_one_ulp_off_refuses_and_negative_zero_passes():
     z[7] = -0.0  # depth > 0 and depth - z treat -0.0 and 0.0 alike
     ok, out = _conv(z)
     assert ok and not out.any()
+
+
+def test_concurrent_callers_keep_their_own_verdicts():
+    """Round-5 advisor finding: the copy pool is one per process and several threads may drive
+    handles at once (ctypes releases the GIL).  A job's 'not exact millimetres' flag belongs to that
+    job: exact and inexact frames converted from four threads at once each get their own answer."""
+    import threading
+    rng = np.random.default_rng(7)
+    good = rng.integers(0, 65536, 640 * 480).astype(np.float64) / 1000.0
+    bad = good.copy()
+    bad[123456] += 1e-7
+    errors = []
+
+    def worker(t):
+        for i in range(60):
+            use_bad = (i + t) % 3 == 0
+            ok, out = _conv(bad if use_bad else good)
+            if ok == use_bad or (ok and not np.array_equal(out, np.round(good * 1000.0).astype(np.uint16))):
+                errors.append((t, i, ok))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors

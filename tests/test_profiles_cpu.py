@@ -137,3 +137,18 @@ def test_hash_profile_takes_the_inserting_window():
         ins, rep = sp.hash_windows(p)
     assert [r["FETCH_SIZE"] for r in ins] == [100.0 + i for i in range(K)]
     assert [r["FETCH_SIZE"] for r in rep] == [200.0 + i for i in range(K)]
+
+
+def test_load_sweep_attached_only_for_its_build(bench, tmp_path):
+    """config[2]'s load-factor sweep rides in the hash block only for the library build it measured."""
+    pt = {"slots": 1 << 19, "target_load": 0.75, "load_window_end": 0.75,
+          "inserting": {"kernel_avg_us": 1460.0, "over_dense": 1.10, "over_load_0_1": 1.0, "mean_probe": 2.7,
+                        "max_probe": 95, "tombstones_after": 2190},
+          "repeat": {"kernel_avg_us": 1418.0}}
+    p = tmp_path / "sweep.json"
+    p.write_text(json.dumps({"build_id": "abc", "workload": "w", "dense_same_extent": {"async": {"kernel_avg_us": 1325.0}},
+                             "sweep": [pt]}))
+    got = bench.load_sweep("abc", str(p))
+    assert got["points"][0]["inserting_over_dense"] == 1.10 and got["dense_same_extent_kernel_us"] == 1325.0
+    assert "measured library build abc, this is xyz" in bench.load_sweep("xyz", str(p))["note"]
+    assert "no " in bench.load_sweep("abc", str(tmp_path / "none.json"))["note"]

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -302,10 +303,27 @@ static bool depth_mm_any(unsigned short* dst, const double* src, size_t n) {
 // Host copies into the page-locked bounce slots (ingest and the deferred drop-in frames) by a
 // persistent pool of copy threads: one 640x480 f64 depth frame is 2.4 MB, and a single-thread
 // memcpy of it and its colour (~140 us) bounded the per-frame drop-in rate (6k frames/s; 10k
-// with the pool); spawning threads per call cost more than it saved below 4 MB.  The caller copies one share itself; the workers wake
-// on a generation counter.  TSDF_COPY_THREADS sets the pool size (0: copy on the calling thread).
-// The pool also runs the deferred frames' depth conversion (depth_mm_any), share by share.
+// with the pool); spawning threads per call cost more than it saved below 4 MB.  The caller copies
+// one share itself.  A deferred frame is ONE job -- its depth (converted to u16 millimetres, or
+// copied) and its colour, share by share -- so a frame costs one hand-off, and the workers spin on
+// the job counter for a while after each job (TSDF_COPY_SPIN_US, 300 us by default) before they
+// block: at the reference's one-call-per-frame rate (~100 us apart) they never sleep, so no frame
+// waits for a thread to wake (round 5 handed each frame over twice through a condition variable,
+// and the per-frame rate varied from 4.7k to 12.3k frames/s between boxes).
+// TSDF_COPY_THREADS sets the pool size (0: copy on the calling thread).
 namespace {
+// Up to two parts, each split into the same number of shares: part a copies a_n bytes (kind 0) or
+// converts a_n f64 depth values to u16 millimetres (kind 1, depth_mm_any); part b copies b_n bytes.
+struct CopyJob {
+    int a_kind = 0;
+    char* a_dst = nullptr;
+    const char* a_src = nullptr;
+    size_t a_n = 0;
+    char* b_dst = nullptr;
+    const char* b_src = nullptr;
+    size_t b_n = 0;
+};
+
 class CopyPool {
   public:
     static CopyPool& get() {
@@ -316,94 +334,102 @@ class CopyPool {
         return *pool;                                                  //  the parent's pool is left)
     }
     void copy(void* dst, const void* src, size_t bytes) {
-        const int nw = (int)workers_.size();
-        if (nw == 0 || bytes < (256u << 10)) {
+        if (workers_.empty() || bytes < (256u << 10)) {
             std::memcpy(dst, src, bytes);
             return;
         }
-        run_job(0, dst, src, bytes, 64);
+        CopyJob j;
+        j.a_dst = (char*)dst, j.a_src = (const char*)src, j.a_n = bytes;
+        run_job(j);
     }
     bool depth_mm(unsigned short* dst, const double* src, size_t n) {  // depth_mm_any over the pool
         if (workers_.empty() || n < (32u << 10)) return depth_mm_any(dst, src, n);
-        return run_job(1, dst, src, n, 64);
+        CopyJob j;
+        j.a_kind = 1, j.a_dst = (char*)dst, j.a_src = (const char*)src, j.a_n = n;
+        return run_job(j);
+    }
+    // One deferred frame: its depth converted (convert: n_depth f64 values -> u16 at ddst; false
+    // when a value is not exact millimetres) or copied (n_depth bytes), and its colour copied.
+    bool frame(bool convert, void* ddst, const void* dsrc, size_t n_depth, void* cdst, const void* csrc,
+               size_t c_bytes) {
+        CopyJob j;
+        j.a_kind = convert ? 1 : 0, j.a_dst = (char*)ddst, j.a_src = (const char*)dsrc, j.a_n = n_depth;
+        j.b_dst = (char*)cdst, j.b_src = (const char*)csrc, j.b_n = c_bytes;
+        if (workers_.empty()) return share(j, 0, 1);
+        return run_job(j);
     }
 
   private:
-    // job 0: copy `n` bytes; job 1: convert `n` depth values; shares of `chunk` units (a multiple
-    // of `align`), share 0 on the calling thread.  Returns false when a share of a conversion
-    // found a value that is not exact millimetres: the flag belongs to the job -- cleared and read
-    // under call_, so a concurrent caller (handles driven from several threads: ctypes releases
-    // the GIL) can neither clear another job's flag nor see it (round-5 advisor finding)
-    bool run_job(int job, void* dst, const void* src, size_t n, size_t align) {
-        const int nw = (int)workers_.size();
+    // the job's shares: share 0 on the calling thread, share k on worker k.  The job's flag (a value
+    // that is not exact millimetres) belongs to the job: cleared and read under call_, so a
+    // concurrent caller (handles driven from several threads: ctypes releases the GIL) can neither
+    // clear another job's flag nor see it (round-5 advisor finding)
+    bool run_job(const CopyJob& j) {
         std::lock_guard<std::mutex> call(call_);  // one job at a time through the pool
-        bad_ = 0;
-        const size_t parts = (size_t)nw + 1;
-        const size_t chunk = ((n + parts - 1) / parts + align - 1) / align * align;
-        {
+        job_ = j;
+        bad_.store(0, std::memory_order_relaxed);
+        left_.store((int)workers_.size(), std::memory_order_relaxed);
+        gen_.fetch_add(1, std::memory_order_seq_cst);  // publishes job_
+        if (sleepers_.load(std::memory_order_seq_cst) > 0) {
             std::lock_guard<std::mutex> g(m_);
-            job_ = job;
-            dst_ = (char*)dst;
-            src_ = (const char*)src;
-            bytes_ = n;
-            chunk_ = chunk;
-            left_ = nw;
-            ++gen_;
+            cv_.notify_all();
         }
-        cv_.notify_all();
-        share(job, (char*)dst, (const char*)src, n, chunk, 0);
-        std::unique_lock<std::mutex> g(m_);
-        done_.wait(g, [&] { return left_ == 0; });
-        return bad_ == 0;  // (every share has finished: the workers' flags are in)
+        const bool ok0 = share(job_, 0, (int)workers_.size() + 1);
+        while (left_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+        return ok0 && bad_.load(std::memory_order_relaxed) == 0;
     }
-    void share(int job, char* d, const char* s, size_t n, size_t chunk, int k) {
-        const size_t o = (size_t)k * chunk;
-        if (o >= n) return;
-        const size_t len = std::min(chunk, n - o);
-        if (job == 0) {
-            std::memcpy(d + o, s + o, len);
-        } else if (!depth_mm_any((unsigned short*)d + o, (const double*)s + o, len)) {
-            bad_ = 1;
+    static size_t chunk_of(size_t n, int parts) { return ((n + parts - 1) / parts + 63) / 64 * 64; }
+    bool share(const CopyJob& j, int k, int parts) {
+        bool ok = true;
+        const size_t ca = chunk_of(j.a_n, parts), oa = (size_t)k * ca;
+        if (oa < j.a_n) {
+            const size_t len = std::min(ca, j.a_n - oa);
+            if (j.a_kind == 0) std::memcpy(j.a_dst + oa, j.a_src + oa, len);
+            else ok = depth_mm_any((unsigned short*)j.a_dst + oa, (const double*)j.a_src + oa, len);
         }
+        const size_t cb = chunk_of(j.b_n, parts), ob = (size_t)k * cb;
+        if (ob < j.b_n) std::memcpy(j.b_dst + ob, j.b_src + ob, std::min(cb, j.b_n - ob));
+        return ok;
     }
     CopyPool() : pid_(getpid()) {
         // two workers (three shares): 12.3k frames/s per-frame dense drop-in against 7.2k on the
-        // calling thread alone; four or eight were no faster and dipped more often
-        // (tools/gpu/dropin_rate.py, profiles/r02_dropin_copy_threads.txt)
+        // calling thread alone (tools/gpu/dropin_rate.py, profiles/r02_dropin_copy_threads.txt;
+        // round 6's sizes: profiles/r06_dropin/)
         int n = (int)std::min(2u, std::max(1u, std::thread::hardware_concurrency() / 2));
         if (const char* e = getenv("TSDF_COPY_THREADS")) n = std::max(0, std::min(32, atoi(e)));
+        if (const char* e = getenv("TSDF_COPY_SPIN_US")) spin_us_ = std::max(0, atoi(e));
         for (int i = 0; i < n; ++i) workers_.emplace_back([this, i] { run(i + 1); });
         for (auto& t : workers_) t.detach();  // live for the process
     }
     void run(int k) {
         unsigned long long seen = 0;
         for (;;) {
-            int job;
-            char* d;
-            const char* s;
-            size_t n, chunk;
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return gen_ != seen; });
-                seen = gen_;
-                job = job_, d = dst_, s = src_, n = bytes_, chunk = chunk_;
+            // the next job: spin for spin_us_, then block until it is published
+            const auto t0 = std::chrono::steady_clock::now();
+            for (unsigned it = 1; gen_.load(std::memory_order_acquire) == seen; ++it) {
+                __builtin_ia32_pause();
+                if ((it & 255) == 0 &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+                    sleepers_.fetch_add(1, std::memory_order_seq_cst);
+                    std::unique_lock<std::mutex> g(m_);
+                    cv_.wait(g, [&] { return gen_.load(std::memory_order_seq_cst) != seen; });
+                    sleepers_.fetch_sub(1, std::memory_order_seq_cst);
+                }
             }
-            share(job, d, s, n, chunk, k);
-            std::lock_guard<std::mutex> g(m_);
-            if (--left_ == 0) done_.notify_one();
+            seen = gen_.load(std::memory_order_acquire);
+            const CopyJob j = job_;  // (written before gen_ moved; the caller waits for every share)
+            if (!share(j, k, (int)workers_.size() + 1)) bad_.store(1, std::memory_order_relaxed);
+            left_.fetch_sub(1, std::memory_order_release);
         }
     }
     pid_t pid_;
     std::vector<std::thread> workers_;
     std::mutex call_, m_;
-    std::condition_variable cv_, done_;
-    int job_ = 0;
-    char* dst_ = nullptr;
-    const char* src_ = nullptr;
-    size_t bytes_ = 0, chunk_ = 0;
-    int left_ = 0;
-    unsigned long long gen_ = 0;
-    std::atomic<int> bad_{0};
+    std::condition_variable cv_;
+    CopyJob job_;
+    std::atomic<unsigned long long> gen_{0};
+    std::atomic<int> left_{0}, bad_{0}, sleepers_{0};
+    int spin_us_ = 300;
 };
 }  // namespace
 
@@ -579,23 +605,26 @@ int Base::defer_push(const void* depth, int dk, const void* color, int ck, int H
     // quarter of the bytes into the bounce slot and over PCIe, the same metres in the kernels
     // (depth_mm_any); a batch holds one kind, so a frame that does not convert after u16 ones
     // sends the caller back to flush them first (kDeferFlush), and then starts an f64 batch
-    // (after such a frame the next kMmBackoff batches go as f64 without trying: mm_backoff)
-    bool staged = false;
+    // (after such a frame the next kMmBackoff batches go as f64 without trying: mm_backoff).  The
+    // depth and the colour go through the copy pool as one job.
     const bool try_mm = i == 0 ? mm_backoff == 0 : dfr.dk == TSDF_DEPTH_U16_MM;
     if (i == 0 && mm_backoff > 0) --mm_backoff;
+    char* const cdst = (char*)hst_color[dfr.slot] + cbytes * i;
     if (dk == TSDF_DEPTH_F64_M && defer_mm && try_mm) {
-        if (CopyPool::get().depth_mm((unsigned short*)hst_depth[dfr.slot] + npx * i, (const double*)depth, npx)) {
+        if (CopyPool::get().frame(true, (unsigned short*)hst_depth[dfr.slot] + npx * i, depth, npx, cdst, color,
+                                  cbytes)) {
             dfr.dk = TSDF_DEPTH_U16_MM;
-            staged = true;
         } else {
             mm_backoff = kMmBackoff;
             if (i > 0) return kDeferFlush;
-            dfr.dk = TSDF_DEPTH_F64_M;
+            dfr.dk = TSDF_DEPTH_F64_M;  // (the colour is in place: copy the depth as it is)
+            CopyPool::get().copy(hst_depth[dfr.slot], depth, frame_bytes_depth(dfr.dk, H, W));
         }
+    } else {
+        const size_t db = frame_bytes_depth(dfr.dk, H, W);
+        CopyPool::get().frame(false, (char*)hst_depth[dfr.slot] + db * i, depth, db, cdst, color, cbytes);
     }
     const size_t dbytes = frame_bytes_depth(dfr.dk, H, W);
-    if (!staged) par_memcpy((char*)hst_depth[dfr.slot] + dbytes * i, depth, dbytes);
-    par_memcpy((char*)hst_color[dfr.slot] + cbytes * i, color, cbytes);
     std::memcpy(dfr.T + 16 * i, T, 16 * sizeof(double));
     dfr.ow[i] = ow;
     dfr.n = i + 1;

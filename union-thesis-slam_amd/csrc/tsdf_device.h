@@ -1085,6 +1085,23 @@ constexpr int kCullWG = 512;  // k_cull: 8 waves, wave w culls frames w and w + 
 // The cull's wave then initialises its new blocks -- (1, 0, 0) and no entries, 64 lanes per block --
 // and records them for k_free_unused (a block the batch leaves without an entry is freed at the end
 // of the call).  kResFail: the pool or table is full (the brick goes to the host's exact re-run).
+#ifndef TSDF_CULL_PROBE8  // cull_find_or_insert walks the table 8 slots per dependent load (round 6)
+#define TSDF_CULL_PROBE8 1  // instead of one (0: round 5's lane-serial probe, for A/B)
+#endif
+// A block taken from the pool for a key whose probe then ended without inserting it (the table ran
+// out of slots after a lost race): recorded in the inserted list as -2 - block, so k_free_unused
+// returns it to the free list at the end of the call (round-5 advisor: it stayed counted as used).
+__device__ inline void spare_block(const Table& t, int blk) {
+    if (blk < 0) return;
+    const unsigned long long k = atomicAdd((unsigned long long*)&t.st->n_inserted, 1ull);
+    if ((long long)k < t.ins_cap) t.ins_list[k] = -2 - blk;
+}
+__device__ inline void cull_probe_stats(unsigned long long* s_stat, long long n, bool alloc) {
+    if (alloc) atomicAdd(&s_stat[ST_ALLOC], 1ull);
+    atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
+    atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
+    atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
+}
 __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned e, unsigned long long* s_stat,
                                           bool& fresh) {
     fresh = false;
@@ -1097,15 +1114,92 @@ __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned
     const long long cap = t.capacity, max_blocks = t.max_blocks;
     const long long mask = cap - 1;
     long long s = ref_hash<true>(bx, by, bz, cap, t.int_bits);
-    long long tomb = -1;
+    long long tomb = -1, tomb_n = 0;
     int blk = -1;
-    for (long long n = 0; n < cap; ++n) {
+#if TSDF_CULL_PROBE8
+    if (cap >= 8) {
+        // Eight slots per step: the aligned 64-B group of keys holding slot s (four 16-B loads) and
+        // its 32 B of slot values, issued together -- one memory latency per 8 slots instead of one
+        // per slot, so a lane's chain at a high load factor is an eighth as long (the wave waits for
+        // its longest).  Plain loads: in this launch a key only ever goes from empty / tombstone to
+        // a key (no removal runs beside the cull), and this brick's key is inserted by no one but
+        // this lane, so a stale read can only show an empty / tombstone slot that another brick has
+        // just taken -- its CAS then fails and the probe goes on, as on a lost race; a key from an
+        // earlier launch (and its value) is visible from the launch's start.
+        for (long long n = 0; n < cap;) {
+            const long long g0 = s & ~7ll;
+            const int off = (int)(s - g0);
+            unsigned long long kk[8];
+            int vv[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const ulonglong2 q = *(const ulonglong2*)(keys + g0 + 2 * j);
+                kk[2 * j] = q.x;
+                kk[2 * j + 1] = q.y;
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int4 q = *(const int4*)(vals + g0 + 4 * j);
+                vv[4 * j] = q.x, vv[4 * j + 1] = q.y, vv[4 * j + 2] = q.z, vv[4 * j + 3] = q.w;
+            }
+            unsigned hit = 0, emp = 0, tm = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                hit |= (unsigned)(kk[i] == key) << i;
+                emp |= (unsigned)(kk[i] == kEmpty) << i;
+                tm |= (unsigned)(kk[i] == kTomb) << i;
+            }
+            const unsigned from = 0xFFu << off;  // the slots at or after s
+            const unsigned stop = (hit | emp) & from;
+            const int i = stop ? __builtin_ctz(stop) : 8;  // the first key match or empty slot
+            const unsigned before = tm & from & ((1u << i) - 1u);  // tombstones before it
+            if (tomb < 0 && before) {
+                tomb = g0 + __builtin_ctz(before);
+                tomb_n = n + (__builtin_ctz(before) - off);
+            }
+            if (i == 8) {  // no stop in the group: on to the next
+                n += 8 - off;
+                s = (g0 + 8) & mask;
+                continue;
+            }
+            long long vi = 0;  // vv[i] without a dynamically indexed register array
+#pragma unroll
+            for (int j = 0; j < 8; ++j) vi = j == i ? vv[j] : vi;
+            if ((hit >> i) & 1u) {
+                cull_probe_stats(s_stat, n + (i - off), false);
+                spare_block(t, blk);  // (never holds one: only this lane inserts this key)
+                return (vi >= 0 && vi < max_blocks) ? (int)vi : kResFail;  // (a found key's value is always set)
+            }
+            // absent: a block from the pool (kept across lost races), then the key by CAS into the
+            // first tombstone of the probe, else this empty slot
+            const long long target = tomb >= 0 ? tomb : g0 + i;
+            const long long tn = tomb >= 0 ? tomb_n : n + (i - off);
+            const unsigned long long expect = tomb >= 0 ? kTomb : kEmpty;
+            if (blk < 0) blk = pool_alloc(t);
+            if (blk < 0) return kResFail;  // pool exhausted
+            if (atomicCAS(&keys[target], expect, key) == expect) {
+                coh_store(&vals[target], blk);
+                const unsigned long long k = atomicAdd((unsigned long long*)&t.st->n_inserted, 1ull);
+                if ((long long)k < t.ins_cap) t.ins_list[k] = (int)e;
+                cull_probe_stats(s_stat, tn, true);
+                fresh = true;
+                return blk;
+            }
+            // another brick's key took the slot: probe on just past it
+            n = tn + 1;
+            s = (target + 1) & mask;
+            tomb = -1;
+        }
+        spare_block(t, blk);
+        return kResFail;  // table full (the growth policy keeps it below 31/32)
+    }
+#endif
+    for (long long n = 0; n < cap; ++n) {  // one slot per step (tables of < 8 slots; A/B)
         const unsigned long long k = coh_load(&keys[s]);
         if (k == key) {
             const int b = coh_load(&vals[s]);
-            atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
-            atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
-            atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
+            cull_probe_stats(s_stat, n, false);
+            spare_block(t, blk);
             return (b >= 0 && b < max_blocks) ? b : kResFail;  // (a found key's value is always set)
         }
         if (k == kTomb) {
@@ -1119,10 +1213,7 @@ __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned
                 coh_store(&vals[target], blk);
                 const unsigned long long i = atomicAdd((unsigned long long*)&t.st->n_inserted, 1ull);
                 if ((long long)i < t.ins_cap) t.ins_list[i] = (int)e;
-                atomicAdd(&s_stat[ST_ALLOC], 1ull);
-                atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
-                atomicAdd(&s_stat[ST_PROBE], (unsigned long long)n);
-                atomicMax(&s_stat[ST_PROBE_MAX], (unsigned long long)n);
+                cull_probe_stats(s_stat, n, true);
                 fresh = true;
                 return blk;
             }
@@ -1132,6 +1223,7 @@ __device__ inline int cull_find_or_insert(const Vol& v, const Table& t, unsigned
         }
         s = (s + 1) & mask;
     }
+    spare_block(t, blk);
     return kResFail;  // table full (the growth policy keeps it below 31/32)
 }
 

@@ -434,6 +434,11 @@ __global__ void k_free_unused(Vol v, Table t) {
     const int nb12 = v.nb[1] * v.nb[2];
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const int e = t.ins_list[i];
+        if (e < 0) {  // a spare block of a probe that ran out of slots (spare_block): back to the free list
+            const unsigned long long f = atomicAdd((unsigned long long*)&t.st->free_count, 1ull);
+            coh_store(&t.free_list[f], -2 - e);
+            continue;
+        }
         const int bx = e / nb12, r = e - bx * nb12, by = r / v.nb[2], bz = r - by * v.nb[2];
         const long long s = probe_find(t, pack_key(bx, by, bz), ref_hash(bx, by, bz, t.capacity, t.int_bits));
         if (s < 0) continue;
@@ -766,20 +771,6 @@ long long next_pow2(long long n) {
     return p;
 }
 
-// The overflow re-run's doubling (hash_after_batch: a brick found no slot): the API size and the
-// device slots together -- bounded like table_room's, so a table that stays full for another
-// reason fails with TSDF_E_CAPACITY instead of doubling until the device is out of memory.
-int grow_table(tsdf_hash* h) {
-    const long long bound = std::max<long long>(next_pow2(h->map_size),
-                                                next_pow2((long long)(2.0 * (double)h->b.n_bricks / h->max_load) + 64));
-    if (next_pow2(2 * h->map_size) > bound)
-        return set_error(TSDF_E_CAPACITY, "hash table: a table of %lld slots for %lld bricks is full; not doubling "
-                         "further", (long long)h->t.capacity, (long long)h->b.n_bricks);
-    TSDF_TRY(resize_table(h, next_pow2(2 * h->map_size)));
-    h->map_size *= 2;
-    return TSDF_OK;
-}
-
 // The tombstone count of a pool report of launch `seq`, or 0 when that launch ran on a table that
 // has since been rebuilt (rehash_seq): the rebuild cleared those tombstones.  Round 5 took the max
 // of the estimate and every report, so a report written just before a rebuild brought the old
@@ -802,9 +793,12 @@ long long table_tombs(const tsdf_hash* h, long long seq, long long report_tombs)
 // 5's OOM).
 int table_room(tsdf_hash* h, long long live, long long extra, long long tombs, bool slots_room = false) {
     const long long nb = h->b.n_bricks;
-    if (live < 0 || live > nb || tombs < 0 || tombs > h->t.capacity)
+    if (live < 0 || live > nb || tombs < 0)
         return set_error(TSDF_E_CAPACITY, "hash table: implausible counts (%lld live keys, %lld tombstones) for %lld "
                          "bricks and %lld slots", live, tombs, nb, (long long)h->t.capacity);
+    // (the tombstone count is an upper bound -- it counts key -> tombstone transitions since the
+    // last rebuild, and a slot can take several -- but no more slots than the table has)
+    tombs = std::min<long long>(tombs, h->t.capacity);
     extra = std::max<long long>(0, std::min<long long>(extra, nb - live));
     const long long bound = std::max<long long>(h->map_size, (long long)(2.0 * (double)nb / h->max_load) + 64);
     long long ms = h->map_size;
@@ -968,10 +962,19 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
         }
         TSDF_HIP(hipMemcpyAsync(h->d_list, h->t.overflow, sizeof(ListEntry) * n_ov, hipMemcpyDeviceToDevice, B.stream));
         TSDF_HIP(hipMemsetAsync(&h->t.st->n_overflow, 0, sizeof(long long), B.stream));
-        if (h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count)
-            TSDF_TRY(grow_pool(h, pool_target(h, h->host_st.pool_top + 2 * n_ov)));
-        else
-            TSDF_TRY(grow_table(h));
+        // Grow what ran short.  A brick is skipped when its block found no slot (the table) or no
+        // pool block; the fused cull of batch L ran in launch L-1 with the pool limit of then, so
+        // after the previous batch's check grew the pool its skips find room now and need no
+        // growth -- round 5 charged them to the table and doubled it for every such batch (the
+        // sweep's fresh 2^22-slot tables hit table_room's bound on it).  A re-run
+        // that still skips grows the pool past its limit.
+        const long long live = h->host_st.pool_top - h->host_st.free_count;
+        const bool pool_short = h->host_st.pool_top + n_ov > h->t.max_blocks - h->host_st.free_count;
+        const bool table_short = live + h->host_st.tombs + n_ov >= h->t.capacity - h->t.capacity / 32;
+        if (pool_short || (round > 0 && !table_short))
+            TSDF_TRY(grow_pool(h, pool_target(h, std::max<long long>(h->host_st.pool_top + 2 * n_ov,
+                                                                       h->t.max_blocks + n_ov))));
+        if (table_short) TSDF_TRY(table_room(h, live, n_ov, h->host_st.tombs, true));
         launch_integrate(h, bt, dk, ck, h->d_list, nullptr, (int)n_ov);
         TSDF_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, B.stream, h->t.st, (long long)h->t.max_blocks,
@@ -988,7 +991,7 @@ int hash_after_batch(tsdf_hash* h, const Batch& bt, int dk, int ck) {
 // and preps L+2.  Synchronous calls check batch L's overflow before launch L+1 is issued; its
 // re-run reads batch L's frames, which no launch has replaced.
 // Invariant: block ids stay fixed between the cull that writes a claim word and the integrate that
-// reads it.  What the host may run in between keeps them: grow_table rehashes keys, never values;
+// reads it.  What the host may run in between keeps them: a table resize rehashes keys, never values;
 // grow_pool maps or copies blocks in place; an overflow re-run only updates or inserts blocks, and
 // the integrate loads every block it is given (a block the cull inserted may have been updated by
 // that re-run).  A future step that renumbers blocks between launches must rerun the cull.  Blocks
