@@ -10,6 +10,7 @@
 #   abs:<reps>:<a,b,..> tools/gpu/ab.sh: the bench and rank 0 of eighth dense / hash shards, per build
 #                      ("base", abtest/lib<name>.so, or VAR=VAL[+VAR2=VAL2] on the in-tree library)
 #   bench[@tag][:<args>]  bench.py --gpus 1 --steps 20 --warmup 5 [args, '+'-separated] -> bench[_tag].json
+#   gloo2[:<args>]     bench.py --gpus 2 --dist-backend gloo (two ranks on the one GPU) -> bench_gpus2_gloo.json
 #   sq[:<lib>]         one rocprofv3 --pmc SQ pass over the dense + hash bench legs
 #   prof               the round profile (tools/gpu/run_round_prof.sh)
 #   py:<script>[:args] python tools/gpu/<script> [args, '+'-separated]
@@ -61,6 +62,12 @@ for step in "$@"; do
       IFS=: read -r _ reps names <<< "$step"
       IFS=, read -ra libs <<< "$names"
       bash tools/gpu/ab.sh "$O/abs" "$reps" "${libs[@]}" > "$O/abs.out" 2>&1 || exit 1
+      ;;
+    gloo2*)
+      # gloo2[:args]: the bench's multi-rank path, two ranks sharing the one GPU over gloo
+      args=""; [[ $step == *:* ]] && args=${step#*:}; args=${args//+/ }
+      timeout -k 10 600 python bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 $args \
+        > "$O/bench_gpus2_gloo.json" 2> "$O/bench_gpus2_gloo.err" || exit 1
       ;;
     bench*)
       # bench[@tag][:args]: output <dir>/bench[_tag].json

@@ -11,7 +11,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                                 "union-thesis-slam_amd"))
-from tsdf_amd import grid_fusion, hash_fusion, scene  # noqa: E402
+from tsdf_amd import _ffi, grid_fusion, hash_fusion, scene  # noqa: E402
 
 
 def main():
@@ -23,7 +23,8 @@ def main():
     d64 = d.cpu().numpy().view(np.uint16).astype(np.float64) / 1000.0
     ch = c.cpu().numpy()
     K = scene.intrinsics()
-    out = {"copy_threads": os.environ.get("TSDF_COPY_THREADS", "default")}
+    out = {"copy_threads": os.environ.get("TSDF_COPY_THREADS", "default"), "build_id": _ffi.build_id(),
+           "copy_spin_us": os.environ.get("TSDF_COPY_SPIN_US", "default")}
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else [None]
     for rep in range(2 if modes[0] is not None else 1):
         for mode in modes:

@@ -107,6 +107,8 @@ def main():
     for k, v in out.items():
         n = int(k.lstrip("slabcyclic"))
         v["predicted_efficiency"] = round(v["fps"] / (n * base), 3)
+    from tsdf_amd import _ffi
+    out["build_id"] = _ffi.build_id()
     print(json.dumps(out))
 
 
@@ -160,6 +162,8 @@ def hash_shards(a, timed, bnds):
         for k, v in out.items():
             if k.startswith("hash"):
                 v["predicted_efficiency"] = round(v["fps"] / (int(k[4:]) * base), 3)
+    from tsdf_amd import _ffi
+    out["build_id"] = _ffi.build_id()
     print(json.dumps(out))
 
 
