@@ -67,11 +67,14 @@ typedef struct {
     int64_t frames;           /* frames integrated */
     int64_t voxel_updates;    /* sum over frames of V_f (voxels whose tsdf/weight/colour changed) */
     int64_t bricks_visited;   /* bricks that passed the conservative frustum/depth cull */
-    int64_t bricks_touched;   /* bricks with >= 1 updated voxel (B_f summed) */
+    int64_t bricks_touched;   /* bricks with >= 1 updated voxel, summed over launches; the fused
+                                 launches count each z-half wave that updated a voxel (up to two
+                                 per brick) -- per-block counts: lookups */
     int64_t blocks_allocated; /* hash: blocks newly allocated */
     int64_t probe_steps;      /* hash: total linear-probe distance of block lookups */
     int64_t probe_max;        /* hash: longest probe distance seen */
-    int64_t lookups;          /* hash: block lookups performed */
+    int64_t lookups;          /* hash: block lookups performed (fused launches: one per kept
+                                 block per launch, by the cull's find-or-insert) */
     double kernel_ms;         /* integrate-kernel time from HIP events (profiling on only) */
     int64_t kernel_launches;  /* integrate-kernel launches timed */
     int64_t bricks_skipped;   /* hash: bricks a launch skipped for lack of table/pool space --
@@ -147,7 +150,7 @@ int tsdf_dense_integrate_batch(tsdf_dense_t* h, int n_frames, const void* depth,
 int tsdf_dense_get(tsdf_dense_t* h, float* tsdf, float* weight, float* color);
 int tsdf_dense_set(tsdf_dense_t* h, const float* tsdf, const float* weight, const float* color);
 int tsdf_dense_sync(tsdf_dense_t* h);
-/* Frames one launch integrates (the temporal batch: 16 in this build, 8 with -DTSDF_MAX_BATCH=8;
+/* Frames one launch integrates (the temporal batch: 32 in this build, 16 or 8 with -DTSDF_MAX_BATCH;
  * TSDF_BATCH overrides per process); calls of n frames run ceil(n / batch) + 2 pipelined launches. */
 int tsdf_dense_frames_per_launch(tsdf_dense_t* h, int* n);
 /* Mesh of the shard's tsdf at level 0 (get_mesh / get_point_cloud, grid_fusion.py:322-360; the
@@ -255,7 +258,7 @@ int tsdf_hash_sync(tsdf_hash_t* h);
 int tsdf_hash_trim(tsdf_hash_t* h);
 int tsdf_hash_stats(tsdf_hash_t* h, tsdf_stats_t* out, int reset);
 int tsdf_hash_set_profiling(tsdf_hash_t* h, int on);
-/* Frames one launch of this table integrates (as tsdf_dense_frames_per_launch: 16 in this build;
+/* Frames one launch of this table integrates (as tsdf_dense_frames_per_launch: 32 in this build;
  * shards of n_shards > 1 always kMaxBatch). */
 int tsdf_hash_frames_per_launch(tsdf_hash_t* h, int* n);
 

@@ -1,6 +1,7 @@
 """Per-frame integrate() rate from host NumPy (the reference's call pattern), several passes, for
 A/B of the host copy path (TSDF_COPY_THREADS):  python tools/gpu/dropin_rate.py [frames] [passes]
 [TSDF_DEFER_MM values, e.g. 1,0: each measured in turn, twice, on fresh handles]"""
+import contextlib
 import json
 import os
 import sys
@@ -33,7 +34,8 @@ def main():
             for name, mk in (("dense", lambda: grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), 0.02)),
                              ("hash", lambda: hash_fusion.HashTable(np.array([[0.0, 10.24]] * 3), 0.02, 1 << 22,
                                                                     max_blocks=1 << 15))):
-                v = mk()
+                with contextlib.redirect_stdout(sys.stderr):  # (the constructors' prints)
+                    v = mk()
                 v.integrate(ch[0], d64[0], K, poses[0])
                 v.sync()
                 rates = []

@@ -392,10 +392,12 @@ class CopyPool {
         return ok;
     }
     CopyPool() : pid_(getpid()) {
-        // two workers (three shares): 12.3k frames/s per-frame dense drop-in against 7.2k on the
-        // calling thread alone (tools/gpu/dropin_rate.py, profiles/r02_dropin_copy_threads.txt;
-        // round 6's sizes: profiles/r06_dropin/)
-        int n = (int)std::min(2u, std::max(1u, std::thread::hardware_concurrency() / 2));
+        // four workers where the host has the cores (two on small hosts): per-frame dense drop-in
+        // on one MI355X box 13.2k frames/s with 2, 17.1k with 4, 18.9k with 6 -- and 12-13k with 8
+        // or 10, past the box's CPU share with the workers spinning (tools/gpu/dropin_rate.py,
+        // profiles/r06_dropin/); 4 keeps the margin
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        int n = (int)std::max(std::min(2u, hw / 2), std::min(4u, hw / 16));
         if (const char* e = getenv("TSDF_COPY_THREADS")) n = std::max(0, std::min(32, atoi(e)));
         if (const char* e = getenv("TSDF_COPY_SPIN_US")) spin_us_ = std::max(0, atoi(e));
         for (int i = 0; i < n; ++i) workers_.emplace_back([this, i] { run(i + 1); });
