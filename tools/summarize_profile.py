@@ -20,12 +20,12 @@ are the timed ones.
 
 FETCH_SIZE/WRITE_SIZE are KiB.  FETCH_SIZE on gfx950 is (TCC_BUBBLE*128 + (RDREQ - BUBBLE - RDREQ_32B)*64
 + RDREQ_32B*32) (rocprofiler-sdk counter_defs.yaml): a 128-B memory-side read request is tallied at 64 B,
-which is the guide's "half of a wide streaming read" -- and the gathers fill L2 lines by requests of
-their own sizes, so no single factor fits a kernel that does both.  The RDREQ pass counts the L2's
-memory-side read requests by size (TCC_EA0_RDREQ_32B / _64B / _128B); the read bytes are
-32*n32 + 64*n64 + 128*n128, checked against known byte counts by tools/gpu/fetch_probe.hip
-(profiles/r06_fetch_probe/).  WRITE_SIZE is exact for 16-B/lane stores.  Both count L2 memory-side
-traffic: Infinity-Cache hits included, so an upper bound on DRAM bytes.
+the guide's "half of a wide streaming read".  Every L2 fill is such a request whatever the access
+width -- 2- and 4-byte gathers included (tools/gpu/fetch_probe.hip, profiles/r06_fetch_probe/) -- so
+the tally is half of this kernel's reads, gathers and state loads alike; the RDREQ pass counts the
+L2's memory-side read requests by size (TCC_EA0_RDREQ_32B / _64B / _128B) and the read bytes are
+32*n32 + 64*n64 + 128*n128, without assuming it.  WRITE_SIZE is exact for 16-B/lane stores.  Both
+count L2 memory-side traffic: Infinity-Cache hits included, so an upper bound on DRAM bytes.
 """
 import csv
 import json
