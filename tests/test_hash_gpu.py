@@ -265,3 +265,48 @@ def test_fused_and_inline_hash_with_growth_match_dense(hf, monkeypatch, n_shards
             for s, o in zip(S[1:], own[1:]):
                 merged[o] = s[k][o]
             assert np.array_equal(merged, G[k]), (pipe, k)
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_hash_at_load_0_9_with_tombstones_matches_dense(hf, monkeypatch, pipe):
+    """BASELINE config[2]'s high-load end on the cull's eight-slot probe (csrc/tsdf_device.h
+    cull_find_or_insert) and on the in-line kernels (TSDF_PIPELINE=0): a power-of-two table is
+    filled to ~0.9 by filler blocks above the room's ceiling (imported without entries: never
+    updated, as in tools/hash_sweep.py), every third of them is then removed again (tombstones on
+    the probe paths, which the inserts reuse), the resize policy lifted so the table keeps its
+    size.  24 frames then insert and update the room's blocks through long probe chains; the state
+    equals the dense grid over the same extent."""
+    from tsdf_amd import grid_fusion, scene
+    monkeypatch.setenv("TSDF_HASH_MAX_LOAD", "0.97")
+    monkeypatch.setenv("TSDF_PIPELINE", pipe)
+    monkeypatch.setenv("TSDF_BATCH", "8")
+    vs, n = 0.08, 24
+    poses = scene.trajectory(n, seed=0, start=300)
+    d, c = scene.render(poses, scene.make_spheres(0), seed=0, start=300)
+    d, c = np.ascontiguousarray(d.numpy()), np.ascontiguousarray(c.numpy())
+    K = scene.intrinsics()
+    Tinv = np.linalg.inv(poses)
+    room = grid_fusion.TSDFVolume(np.array([[0.0, 10.24]] * 3), vs)
+    room.integrate_batch(d, c, K, Tinv)
+    w = room.get_state()[1]
+    live = int((w.reshape(16, 8, 16, 8, 16, 8) > 0).any(axis=(1, 3, 5)).sum())  # the room's blocks
+    S = 4096 if live < 1800 else 8192
+    fill = int(0.9 * S) - live
+    layers = (fill + 255) // 256  # 16 x 16 blocks per layer, from block z 18 (past the ceiling + trunc)
+    bnds = np.array([[0.0, 10.24], [0.0, 10.24], [0.0, (18 + layers) * 8 * vs - 0.5 * vs]])
+    g = grid_fusion.TSDFVolume(bnds.copy(), vs)
+    g.integrate_batch(d, c, K, Tinv)
+    h = hf.HashTable(bnds.copy(), vs, S, max_blocks=fill + live + 512)
+    i = np.arange(fill)
+    fxyz = np.stack([i % 16, (i // 16) % 16, 18 + i // 256], 1).astype(np.int32)
+    h.import_blocks(fxyz, None, None, None, np.zeros((fill, 8), np.uint64))
+    gone = fxyz[::3].astype(np.int64) * 8  # one voxel of each: its empty block is freed (tombstone)
+    h.remove_entries(gone)
+    info = h.info()
+    assert info["tombstones"] > 0 and info["used"] == fill - len(gone)
+    h.integrate_batch(d, c, K, Tinv)
+    info, st = h.info(), h.stats()
+    assert info["slots"] == S and info["used"] >= 0.85 * S - len(gone), info  # kept its size, near full
+    assert st["probe_max"] > 8, st  # chains past one eight-slot group
+    for a, b in zip(g.get_state(), h.get_state()):
+        assert np.array_equal(a, b)
