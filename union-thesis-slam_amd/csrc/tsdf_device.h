@@ -231,6 +231,18 @@ __host__ __device__ inline unsigned long long pack_key(int bx, int by, int bz) {
 
 __device__ inline int lane_id() { return threadIdx.x & 63; }
 
+// The integrate's per-step conditions as wave lane masks straight from the compares
+// (llvm.amdgcn.fcmp / icmp: one v_cmp into an SGPR pair), combined by scalar ANDs / ORs, and turned
+// back into a lane's condition by the inverse ballot (the mask itself drives v_cndmask and exec).
+// A bool carried across basic blocks is otherwise rebuilt from a VGPR for every ballot of it
+// (v_cndmask + v_cmp: ~14 VALU per wave-frame of the dense integrate).  The
+// predicates are LLVM's: the C operators' semantics (a NaN compares false, != is unordered).
+__device__ unsigned long long fcmp64_mask(double a, double b, int pred) __asm("llvm.amdgcn.fcmp.i64.f64");
+__device__ unsigned long long fcmp32_mask(float a, float b, int pred) __asm("llvm.amdgcn.fcmp.i64.f32");
+__device__ unsigned long long icmp32_mask(unsigned a, unsigned b, int pred) __asm("llvm.amdgcn.icmp.i64.i32");
+constexpr int kCmpOGT = 2, kCmpOGE = 3, kCmpOLT = 4, kCmpUNE = 14, kCmpNE = 33, kCmpULT = 36, kCmpSGT = 38;
+__device__ inline bool lane_in(unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 // Shared table metadata (pool state, keys, slot values, entry masks) is read with agent-scope
 // relaxed atomic loads: always a VECTOR load (global_load ... sc1).  A plain load from a
 // wave-uniform address becomes an s_load through the scalar cache, which was measured to
@@ -585,8 +597,9 @@ __device__ unsigned long long g_ddiag[8];
 // masks in SGPR pairs): their combinations and wave ballots are scalar instructions, not VALU.
 template <int DK, int CK, int NZ>
 __device__ __forceinline__ void project_part(double trunc, const Frame& fr, double px, double py,
-                                             const double* pzs, double pz_l, int zoff, bool col_in, int nz,
-                                             unsigned (&cpx)[NZ], double (&diff)[NZ], bool (&ok)[NZ]) {
+                                             const double* pzs, double pz_l, int zoff, unsigned long long colm,
+                                             int nz, unsigned (&cpx)[NZ], double (&diff)[NZ],
+                                             unsigned long long (&okm)[NZ]) {
     constexpr int kPz = NZ < 8 ? NZ : 1;
     // the z term of OpenBLAS's dgemm chain (grid_fusion.py:363-368): exact, it feeds the depth test
     const double a2 = fma(fr.T[9], py, fr.T[8] * px);
@@ -602,7 +615,7 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     // two f64 per step out of the registers live across the gathers
     double zc[NZ];
     int iu[NZ], iv[NZ];
-    bool in[NZ], slow[NZ], any_slow = false;
+    unsigned long long in[NZ], slow[NZ], any_slow = 0;  // lane masks (fcmp64_mask)
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
         const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
@@ -622,22 +635,23 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         const double ux = rint(sx), uy = rint(sy);
         // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
         // but is invalid either way)
-        const bool fine = (fabs(sx - ux) < fr.half_m) & (fabs(sy - uy) < fr.half_m) &
-                          ((int)(__double_as_longlong(z) >> 32) > fr.zmin_hi);
-        in[k] = col_in & (k < nz) & (z > 0.0);
+        const unsigned long long fine = fcmp64_mask(fabs(sx - ux), fr.half_m, kCmpOLT) &
+                                        fcmp64_mask(fabs(sy - uy), fr.half_m, kCmpOLT) &
+                                        icmp32_mask((unsigned)(__double_as_longlong(z) >> 32), (unsigned)fr.zmin_hi, kCmpSGT);
+        in[k] = (k < nz ? colm : 0ull) & fcmp64_mask(z, 0.0, kCmpOGT);
         iu[k] = cvt_i32_sat(ux);
         iv[k] = cvt_i32_sat(uy);
-        slow[k] = in[k] & !fine;
+        slow[k] = in[k] & ~fine;
         any_slow |= slow[k];
     }
     TSDF_DDIAG(0);
-    if (__ballot(any_slow)) {
+    if (any_slow) {
         TSDF_DDIAG(3);
         const double a0 = fma(fr.T[1], py, fr.T[0] * px);  // the reference's x / y chains
         const double a1 = fma(fr.T[5], py, fr.T[4] * px);
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            if (!slow[k]) continue;
+            if (!slow[k] || !lane_in(slow[k])) continue;
             TSDF_DDIAG(2);
             const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
             const double x = fr.T[3] + fma(fr.T[2], pz, a0);
@@ -646,7 +660,7 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
             iv[k] = cvt_i32_sat(rint((y * fr.fy) / zc[k] + fr.cy));
         }
     }
-    bool cand[NZ];
+    unsigned long long cand[NZ];
     unsigned pix[NZ];
     const int W = fr.W, H = fr.H;
 #pragma unroll
@@ -654,8 +668,9 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         // unsigned bounds on the saturated indices (they come from integral, non-NaN values
         // wherever z > 0: the exact path yields NaN only for a non-finite pose, whose z --
         // np.linalg.inv: all NaN -- fails z > 0)
-        cand[k] = in[k] & ((unsigned)iu[k] < (unsigned)W) & ((unsigned)iv[k] < (unsigned)H);
-        pix[k] = cand[k] ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
+        cand[k] = in[k] & icmp32_mask((unsigned)iu[k], (unsigned)W, kCmpULT) &
+                  icmp32_mask((unsigned)iv[k], (unsigned)H, kCmpULT);
+        pix[k] = lane_in(cand[k]) ? __umul24((unsigned)iv[k], (unsigned)W) + (unsigned)iu[k] : 0u;  // v_mad_u32_u24
     }
     // phase 2: gather depth and colour for every step at once, before the depth test, so
     // all the gathers share one memory latency (non-candidates read pixel 0, discarded).  The
@@ -676,8 +691,9 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
         diff[k] = dep[k] - zc[k];
-        const bool dpos = DK == 0 ? draw[k] != 0u : dep[k] > 0.0;  // u16: RN(m / 1000) > 0 iff m > 0
-        ok[k] = cand[k] & dpos & (diff[k] >= -trunc);
+        // u16: RN(m / 1000) > 0 iff m > 0
+        const unsigned long long dpos = DK == 0 ? icmp32_mask(draw[k], 0u, kCmpNE) : fcmp64_mask(dep[k], 0.0, kCmpOGT);
+        okm[k] = cand[k] & dpos & fcmp64_mask(diff[k], -trunc, kCmpOGE);
     }
 }
 
@@ -732,7 +748,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const int bz = rem - by * v.nb[2];
     const int lx = bx * kBrickEdge + (lane >> 3);
     const int ly = by * kBrickEdge + (lane & 7);
-    const bool col_in = lx < v.dims[0] && ly < v.dims[1];
+    const unsigned long long colm = __ballot(lx < v.dims[0] && ly < v.dims[1]);  // the item's columns inside
     const int nz = min(kBrickEdge, v.dims[2] - bz * kBrickEdge) - zoff;  // valid steps of this part
     // vox2world (grid_fusion.py:170-181); lanes 0..7 compute the brick's 8 z coordinates
     const double px = vox_world(v.origin[0], v.vs, v.off[0] + col_gx(v, bx) + (lane >> 3));
@@ -747,8 +763,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 
     // the brick's storage: dense brick b, or its hash pool block (wave-uniform; 32-bit for the hash,
     // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
-    typename std::conditional<HASH, int, long long>::type blk = -1;
+    typename std::conditional<HASH, int, long long>::type blk = HASH ? -1 : b;  // (dense: its brick)
     bool is_new = false;
+    bool upd = false;  // a frame of the batch updates this part (wave-uniform)
     if constexpr (kHalfHash) {
         // the cull's block (written by the previous launch), or kResFail
         const int cur = __builtin_amdgcn_readfirstlane(res[b]);
@@ -777,9 +794,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     // half of a block this launch inserted starts at (1, 0, 0): nothing to load.  Every half held
     // is stored at the end (a changed half, or -- a new hash block -- its init).  Lane masks.
     constexpr int kH = NZ / 4;
-    bool loaded[kH];
+    unsigned long long loaded[kH];  // lane masks
 #pragma unroll
-    for (int h = 0; h < kH; ++h) loaded[h] = false;
+    for (int h = 0; h < kH; ++h) loaded[h] = 0;
     // voxels updated by any frame of the batch (entry bits of the hash, ST_UNIQUE): per z-step,
     // the OR of the step masks' ballots -- scalar registers and scalar ORs, no per-lane VGPR bit field
     unsigned long long touched[NZ] = {};
@@ -800,18 +817,19 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #endif
         unsigned cpx[NZ];
         double diff[NZ];
-        bool okv[NZ];
-        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, zoff, col_in, nz, cpx, diff, okv);
-        bool need[kH];
+        unsigned long long okv[NZ];  // the steps' update masks
+        project_part<DK, CK, NZ>(trunc, fr, px, py, pzs, pz_l, zoff, colm, nz, cpx, diff, okv);
+        unsigned long long need[kH];
 #pragma unroll
         for (int h = 0; h < kH; ++h) need[h] = okv[4 * h] | okv[4 * h + 1] | okv[4 * h + 2] | okv[4 * h + 3];
-        if (__ballot(need[0] | need[kH - 1]) == 0) continue;
+        if ((need[0] | need[kH - 1]) == 0) continue;
         TSDF_DDIAG(1);
 #ifdef TSDF_DIAG
         ++d_valid;
 #endif
 
-        if (!kHalfHash && blk < 0) {  // first frame of the batch that updates this brick: find its storage
+        upd = true;
+        if (HASH && !kHalfHash && blk < 0) {  // first frame of the batch that updates this brick: find its block
             if (HASH) {
                 long long slot = 0, probe = 0;
                 const unsigned long long key = pack_key(bx, by, bz);
@@ -828,7 +846,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 blk = r;
                 if (is_new) {  // a fresh block starts at (1, 0, 0): nothing to load
 #pragma unroll
-                    for (int h = 0; h < kH; ++h) loaded[h] = true;
+                    for (int h = 0; h < kH; ++h) loaded[h] = ~0ull;
                 }
                 if (lane == 0) {
                     atomicAdd(&s_stat[ST_LOOKUPS], 1ull);
@@ -841,18 +859,18 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             }
         }
         // phase 4: state halves not yet in registers (the wave's first frame that needs them)
-        bool ld[kH];
-        bool any_ld = false;
+        unsigned long long ld[kH];
+        unsigned long long any_ld = 0;
 #pragma unroll
         for (int h = 0; h < kH; ++h) {
-            ld[h] = need[h] & !loaded[h];
+            ld[h] = need[h] & ~loaded[h];
             any_ld |= ld[h];
         }
-        if (__ballot(any_ld)) {
+        if (any_ld) {
             const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
 #pragma unroll
             for (int h = 0; h < kH; ++h) {
-                if (!ld[h]) continue;
+                if (!lane_in(ld[h])) continue;
                 const float4 W = *(const float4*)(pool.weight + base + 4 * h);
                 const float4 T = *(const float4*)(pool.tsdf + base + 4 * h);
                 const float4 C = *(const float4*)(pool.color + base + 4 * h);
@@ -888,7 +906,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         for (int h = 0; h < kH; ++h) loaded[h] |= need[h];
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            const unsigned long long m = __ballot(okv[k]);
+            const unsigned long long m = okv[k];
             touched[k] |= m;
             nupd += (unsigned)__popcll(m);  // (wave total, scalar)
         }
@@ -896,6 +914,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
         float wnv[NZ], tqv[NZ], cnv[NZ];  // the step's new weight, tsdf and colour (if it updates)
+        bool ts_same = false;             // (wave-uniform: the fast path's free-space case)
         if (!fast_c) TSDF_DDIAG(5);
         if (fast_c) {
             // Steps in pairs (k, k+1) on the packed f32 ALU (v_pk_*: two lanes' worth per
@@ -908,10 +927,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             // Free space (wave-uniform): every updating voxel is at least trunc in front of the
             // surface (dist = min(1, diff / trunc) = 1 exactly) and still holds tsdf 1, so its new
             // tsdf is (w * 1 + 1) / (w + 1) = 1 exactly: the distance and tsdf quotients are skipped
-            bool busy = false;
+            unsigned long long busy = 0;
 #pragma unroll
-            for (int k = 0; k < NZ; ++k) busy |= okv[k] & ((diff[k] < trunc) | (ts[k] != 1.0f));
-            const bool free_space = __ballot(busy) == 0;
+            for (int k = 0; k < NZ; ++k)
+                busy |= okv[k] & (fcmp64_mask(diff[k], trunc, kCmpOLT) | fcmp32_mask(ts[k], 1.0f, kCmpUNE));
+            const bool free_space = busy == 0;
+            ts_same = free_space;
             if (free_space) TSDF_DDIAG(4);
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
@@ -1009,9 +1030,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         }
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            ws[k] = okv[k] ? wnv[k] : ws[k];
-            ts[k] = okv[k] ? tqv[k] : ts[k];
-            cs[k] = okv[k] ? cnv[k] : cs[k];
+            ws[k] = lane_in(okv[k]) ? wnv[k] : ws[k];
+            cs[k] = lane_in(okv[k]) ? cnv[k] : cs[k];
+        }
+        if (!ts_same) {  // (free space: every tsdf stays as it is -- no selects)
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) ts[k] = lane_in(okv[k]) ? tqv[k] : ts[k];
         }
     }
 #ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
@@ -1025,7 +1049,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #pragma unroll
         for (int k = 0; k < NZ; ++k) any |= touched[k];
         if (any == 0) return;  // this half updated nothing
-    } else if (blk < 0) {
+    } else if (!upd) {
         return;  // no frame of the batch updated this brick
     }
 
@@ -1035,7 +1059,7 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     const size_t base = (size_t)blk * kBrickVox + (size_t)lane * kBrickEdge + zoff;
 #pragma unroll
     for (int h = 0; h < kH; ++h) {
-        if (!loaded[h]) continue;
+        if (!lane_in(loaded[h])) continue;
         *(float4*)(pool.weight + base + 4 * h) = make_float4(ws[4 * h], ws[4 * h + 1], ws[4 * h + 2], ws[4 * h + 3]);
         *(float4*)(pool.tsdf + base + 4 * h) = make_float4(ts[4 * h], ts[4 * h + 1], ts[4 * h + 2], ts[4 * h + 3]);
         if (CU)
