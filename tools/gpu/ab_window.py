@@ -34,8 +34,13 @@ def main():
     Tinv = np.ascontiguousarray(np.linalg.inv(poses))
     K = scene.intrinsics()
     torch.cuda.synchronize()
+    dkind = None
+    if os.environ.get("AB_DEPTH") == "f64":  # the same frames as f64 metres (the integrate's DK = 1 path)
+        depth = (depth.to(torch.int32) & 0xFFFF).to(torch.float64) / 1000.0
+        dkind = _ffi.DEPTH_F64_M
+        name += "_f64"
     dptr, cptr = depth.data_ptr(), rgb.data_ptr()
-    ds, cs = 480 * 640 * 2, 480 * 640 * 3
+    ds, cs = 480 * 640 * depth.element_size(), 480 * 640 * 3
 
     def run(v, start, n, prof, sync=True):
         v.set_profiling(prof)
@@ -47,7 +52,7 @@ def main():
             s %= F
             m = min(left, F - s)
             v.integrate_batch(dptr + s * ds, cptr + s * cs, K, Tinv[s:s + m], hw=(480, 640), device_ptrs=True,
-                              sync=sync)
+                              sync=sync, depth_kind=dkind)
             s += m
             left -= m
         v.sync()

@@ -730,8 +730,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     static_assert(NZ == 8 || NZ == 4, "z-parts of 8 or 4 steps");
     constexpr bool kHalfHash = HASH && NZ == 4;  // (requires res)
     const int lane = lane_id();
-    const int b = (int)(entry & 0xFFFFFFFFull);
-    const unsigned fmask = (unsigned)(entry >> 32);
+    // (wave-uniform: scalar registers, so the frame loop below walks the mask's set bits with
+    // scalar instructions)
+    const int b = __builtin_amdgcn_readfirstlane((int)(entry & 0xFFFFFFFFull));
+    const unsigned fmask = __builtin_amdgcn_readfirstlane((unsigned)(entry >> 32));
     // the volume fields the frame loop reads, once per item (v is re-read per item through an
     // opaque pointer, item_vol: its other fields are not held across the frame loop)
     const double trunc = v.trunc, rtrunc = v.rtrunc;
@@ -759,7 +761,12 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
     constexpr int kPz = NZ < 8 ? NZ : 1;
     double pzs[kPz];
 #pragma unroll
-    for (int k = 0; k < kPz; ++k) pzs[k] = readlane_f64(pz_l, k + zoff);
+    for (int k = 0; k < kPz; ++k) {
+        pzs[k] = readlane_f64(pz_l, k + zoff);
+        // held in VGPRs: an FMA with a frame's scalar operand could not take it from SGPRs (one
+        // scalar operand per VOP3), so the projection would copy it back per frame
+        if (NZ < 8) asm("" : "+v"(pzs[k]));
+    }
 
     // the brick's storage: dense brick b, or its hash pool block (wave-uniform; 32-bit for the hash,
     // where it is one register fewer across the frame loop -- the dense kernel measured faster as is)
@@ -809,9 +816,8 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
 #ifdef TSDF_DIAG
     int d_pairs = 0, d_valid = 0;
 #endif
-    for (int fi = 0; fi < bt.n; ++fi) {
-        if (!((fmask >> fi) & 1u)) continue;
-        const Frame& fr = bt.f[fi];
+    for (unsigned fm = bt.n >= 32 ? fmask : fmask & ((1u << bt.n) - 1u); fm != 0; fm &= fm - 1u) {
+        const Frame& fr = bt.f[__builtin_ctz(fm)];  // the frames that kept this brick, in order
 #ifdef TSDF_DIAG
         ++d_pairs;
 #endif
@@ -949,12 +955,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 }
                 const f2 wn2 = w2 + 1.0f;
                 f2 r2;
-                if (free_space) {
+                if (free_space) {  // (tqv is not read: ts_same)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        tqv[k + j] = ts[k + j];
-                        r2[j] = (float)y[j];
-                    }
+                    for (int j = 0; j < 2; ++j) r2[j] = (float)y[j];
                 } else {
                     const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
 #pragma unroll
