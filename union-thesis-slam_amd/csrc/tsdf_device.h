@@ -242,6 +242,11 @@ __device__ unsigned long long fcmp32_mask(float a, float b, int pred) __asm("llv
 __device__ unsigned long long icmp32_mask(unsigned a, unsigned b, int pred) __asm("llvm.amdgcn.icmp.i64.i32");
 constexpr int kCmpOGT = 2, kCmpOGE = 3, kCmpOLT = 4, kCmpUNE = 14, kCmpNE = 33, kCmpULT = 36, kCmpSGT = 38;
 __device__ inline bool lane_in(unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+// x = lane in m ? y : x, written in place (the register allocator otherwise gives the new value a
+// register of its own and copies it back where the paths merge)
+__device__ inline void sel_in_place(float& x, float y, unsigned long long m) {
+    asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "s"(m));
+}
 
 // Shared table metadata (pool state, keys, slot values, entry masks) is read with agent-scope
 // relaxed atomic loads: always a VECTOR load (global_load ... sc1).  A plain load from a
@@ -635,13 +640,18 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         const double ux = rint(sx), uy = rint(sy);
         // (a NaN fails both tests and takes the exact path; far-out |s| may round differently
         // but is invalid either way)
+        // fine: z > zmin (so z > 0; the high-dword test passes a positive NaN, which then fails
+        // the pixel tests) and both pixel coordinates clear of a rounding boundary.  The other
+        // steps of the column (rare: near a boundary, at or behind the camera plane) take the
+        // z > 0 test and, where it holds, the exact path below
         const unsigned long long fine = fcmp64_mask(fabs(sx - ux), fr.half_m, kCmpOLT) &
                                         fcmp64_mask(fabs(sy - uy), fr.half_m, kCmpOLT) &
                                         icmp32_mask((unsigned)(__double_as_longlong(z) >> 32), (unsigned)fr.zmin_hi, kCmpSGT);
-        in[k] = (k < nz ? colm : 0ull) & fcmp64_mask(z, 0.0, kCmpOGT);
+        const unsigned long long col = k < nz ? colm : 0ull;
+        in[k] = col & fine;
         iu[k] = cvt_i32_sat(ux);
         iv[k] = cvt_i32_sat(uy);
-        slow[k] = in[k] & ~fine;
+        slow[k] = col & ~fine;  // (z > 0 still to test)
         any_slow |= slow[k];
     }
     TSDF_DDIAG(0);
@@ -651,6 +661,8 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
         const double a1 = fma(fr.T[5], py, fr.T[4] * px);
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
+            slow[k] &= fcmp64_mask(zc[k], 0.0, kCmpOGT);
+            in[k] |= slow[k];
             if (!slow[k] || !lane_in(slow[k])) continue;
             TSDF_DDIAG(2);
             const double pz = NZ < 8 ? pzs[k % kPz] : readlane_f64(pz_l, k + zoff);
@@ -919,8 +931,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
         // phase 5: update in registers, straight-line; invalid steps keep their old values.
         // integrate_tsdf (grid_fusion.py:207-212): w f32 <- f64 add; f32 product; f64 average;
         // with obs_weight == 1: f32 w + 1 == f32(f64(w) + 1) exactly, and 1 * dist == dist
-        float wnv[NZ], tqv[NZ], cnv[NZ];  // the step's new weight, tsdf and colour (if it updates)
-        bool ts_same = false;             // (wave-uniform: the fast path's free-space case)
+        // the step's new weight and colour (if it updates); a new tsdf goes into ts at once, so
+        // that no quotient register crosses the branches (free space: no tsdf changes)
+        float wnv[NZ], cnv[NZ];
         if (!fast_c) TSDF_DDIAG(5);
         if (fast_c) {
             // Steps in pairs (k, k+1) on the packed f32 ALU (v_pk_*: two lanes' worth per
@@ -938,8 +951,11 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
             for (int k = 0; k < NZ; ++k)
                 busy |= okv[k] & (fcmp64_mask(diff[k], trunc, kCmpOLT) | fcmp32_mask(ts[k], 1.0f, kCmpUNE));
             const bool free_space = busy == 0;
-            ts_same = free_space;
             if (free_space) TSDF_DDIAG(4);
+            // the pairs' update, instantiated once for free space and once for the general case
+            // (two straight-line paths: nothing of the tsdf's quotients crosses a branch)
+            const auto pairs = [&](auto free_tag) {
+            constexpr bool kFree = decltype(free_tag)::value;
 #pragma unroll
             for (int k = 0; k < NZ; k += 2) {
                 const f2 w2 = {ws[k], ws[k + 1]};
@@ -955,15 +971,15 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 }
                 const f2 wn2 = w2 + 1.0f;
                 f2 r2;
-                if (free_space) {  // (tqv is not read: ts_same)
+                if constexpr (kFree) {
 #pragma unroll
                     for (int j = 0; j < 2; ++j) r2[j] = (float)y[j];
                 } else {
-                    const f2 wt2 = w2 * f2{ts[k], ts[k + 1]};
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const double num = (double)wt2[j] + dist_of(trunc, rtrunc, diff[k + j]);
-                        tqv[k + j] = (float)div_rn(num, (double)wn2[j], y[j]);
+                        const double num = (double)(w2[j] * ts[k + j]) + dist_of(trunc, rtrunc, diff[k + j]);
+                        const float q = (float)div_rn(num, (double)wn2[j], y[j]);
+                        sel_in_place(ts[k + j], q, okv[k + j]);
                         r2[j] = (float)y[j];
                     }
                 }
@@ -995,6 +1011,9 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                     cnv[k + 1] = cn2.y;
                 }
             }
+            };
+            if (free_space) pairs(std::true_type{});
+            else pairs(std::false_type{});
         } else {
             // the exact paths: non-canonical colours or weights (table quotients where the weights
             // allow them, else IEEE divisions)
@@ -1004,9 +1023,10 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const float wn = OW1 ? w_old + 1.0f : (float)((double)w_old + fr.ow);
                 const double dist = dist_of(trunc, rtrunc, diff[k]);
                 const double num = (double)(w_old * ts[k]) + (OW1 ? dist : fr.ow * dist);
-                if (fast_t) tqv[k] = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
-                else if (table_t) tqv[k] = (float)div_rn(num, (double)wn, rcp_hbm[(int)wn]);
-                else tqv[k] = (float)(num / (double)wn);
+                float q;
+                if (fast_t) q = (float)div_rn(num, (double)wn, s_rcp[(int)wn]);
+                else if (table_t) q = (float)div_rn(num, (double)wn, rcp_hbm[(int)wn]);
+                else q = (float)(num / (double)wn);
                 wnv[k] = wn;
                 // colour (grid_fusion.py:302-314): float32 throughout, round half to even
                 float nb, ng, nr;
@@ -1029,16 +1049,13 @@ __device__ inline void integrate_brick(const Vol& v, const Batch& bt, const Pool
                 const float cr = fminf(255.0f, rintf((w_old * orr + (OW1 ? nr : fr.ow32 * nr)) / wn));
                 cnv[k] = CU ? __uint_as_float((unsigned)(cb * 65536.0f + cg * 256.0f + cr))
                             : cb * 65536.0f + cg * 256.0f + cr;
+                ts[k] = lane_in(okv[k]) ? q : ts[k];  // (after every read of the old ts[k])
             }
         }
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
             ws[k] = lane_in(okv[k]) ? wnv[k] : ws[k];
             cs[k] = lane_in(okv[k]) ? cnv[k] : cs[k];
-        }
-        if (!ts_same) {  // (free space: every tsdf stays as it is -- no selects)
-#pragma unroll
-            for (int k = 0; k < NZ; ++k) ts[k] = lane_in(okv[k]) ? tqv[k] : ts[k];
         }
     }
 #ifdef TSDF_DIAG  // dense diagnostics in the hash-only counters: part-frame pairs computed / valid
