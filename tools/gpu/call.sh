@@ -96,8 +96,8 @@ for step in "$@"; do
       ;;
     pylib:*)
       IFS=: read -r _ l script args <<< "$step"
-      TSDF_HIP_LIB=$(lib "$l") timeout -k 10 600 python -u "tools/gpu/$script" ${args//+/ } > "$O/${script%.py}_$l.out" \
-        2> "$O/${script%.py}_$l.err" || exit 1
+      TSDF_HIP_LIB=$(lib "$l") timeout -k 10 600 python -u "tools/gpu/$script" ${args//+/ } >> "$O/${script%.py}_$l.out" \
+        2>> "$O/${script%.py}_$l.err" || exit 1
       ;;
     tool:*)
       IFS=: read -r _ script args tag <<< "$step"
