@@ -4,6 +4,7 @@
 #   tests              pytest -m gpu (in-tree library) + smoke
 #   pytest:<args>      pytest -m gpu <args, '+'-separated> (a subset, e.g. pytest:tests/test_long_gpu.py+-k+config4)
 #   pytestlib:<lib>:<args>  the same with TSDF_HIP_LIB=abtest/lib<lib>.so
+#   testsenv:<VAR=VAL[+..]>  the whole -m gpu suite with that environment (no smoke)
 #   ab:<reps>:<a,b,..> driver-window A/B (tools/gpu/ab_window.py), libraries interleaved <reps>
 #                      times; "base" = in-tree, VAR=VAL[+..] = in-tree with that environment,
 #                      anything else = abtest/lib<name>.so
@@ -38,6 +39,11 @@ for step in "$@"; do
       args=${step#pytest:}; args=${args//+/ }
       timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
         $args > "$O/pytest_subset.log" 2>&1 || { echo "pytest subset failed" >> "$O/steps.log"; exit 1; }
+      ;;
+    testsenv:*)  # the whole GPU suite with VAR=VAL[+VAR2=VAL2] set (e.g. TSDF_TEXEL=1)
+      IFS='+' read -ra envs <<< "${step#testsenv:}"
+      env "${envs[@]}" timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        -p no:cacheprovider > "$O/gpu_tests_env.log" 2>&1 || { echo "tests (env) failed" >> "$O/steps.log"; exit 1; }
       ;;
     pytestlib:*)
       IFS=: read -r _ l args <<< "$step"; args=${args//+/ }

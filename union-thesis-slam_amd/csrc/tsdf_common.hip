@@ -186,6 +186,7 @@ int Base::set_batch(int want) {
     defer_frames = defer_frames < 1 ? 1 : defer_frames > batch ? batch : defer_frames;
     if (const char* e = getenv("TSDF_DEFER_DMA_FRAMES")) dma_grain = atoi(e) < 1 ? 1 : atoi(e);
     if (const char* e = getenv("TSDF_RGB_DIRECT")) rgb_direct = atoi(e) != 0;  // (A/B, parity tests)
+    if (const char* e = getenv("TSDF_TEXEL")) texel_mode = atoi(e) != 0;
     if (const char* e = getenv("TSDF_DEFER_MM")) defer_mm = atoi(e) != 0;
     if (list_set[0]) return TSDF_OK;
     TSDF_HIP(hipMalloc(&list_set[0], sizeof(ListEntry) * (size_t)n_bricks * batch));
@@ -228,7 +229,7 @@ int Base::ensure_pyr(int H, int W) {
     lay = pyr_layout(H, W);
     for (int k = 0; k < n_sets; ++k) {
         TSDF_HIP(hipMalloc(&pyr_set[k], sizeof(float) * (size_t)lay.total * batch));
-        TSDF_HIP(hipMalloc(&rgbx_set[k], sizeof(unsigned) * (size_t)H * W * batch));
+        TSDF_HIP(hipMalloc(&rgbx_set[k], sizeof(unsigned) * 2 * (size_t)H * W * batch));  // (RGBX or texels)
     }
     pyr_H = H;
     pyr_W = W;
@@ -508,6 +509,8 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
     }
     use_set(cur_set);  // (re)read the set's pointers: the buffers above may be new
     bt->n = n;
+    const bool tex = texel_now && dk == TSDF_DEPTH_U16_MM && ck == TSDF_COLOR_RGB8;
+    bt->texel = tex ? 1 : 0;
     for (int i = 0; i < n; ++i) {
         Frame* fr = &bt->f[i];
         const double* T = Tinv + 16 * (size_t)(first + i);
@@ -547,7 +550,8 @@ int Base::prepare_batch(Batch* bt, const void* depth, int dk, const void* color,
         // or a device array with more of the call's frames after this one; else the RGBX copy
         const bool direct = ck == TSDF_COLOR_RGB8 && rgb_direct &&
                             (!(flags & TSDF_DEVICE_PTRS) || (call_color_end && (const char*)fr->color + cbytes < call_color_end));
-        fr->rgbx = direct ? nullptr : rgbx + npx * i;
+        if (tex) fr->rgbx = rgbx + 2 * npx * i;  // the prep's 8-byte texels
+        else fr->rgbx = direct ? nullptr : rgbx + npx * i;
         fr->pyr = pyr + (size_t)lay.total * i;
 
         frustum_planes(fr, T, W, H);

@@ -122,6 +122,13 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
                                   : (int)B.grid_for((const void*)k_fused<true, 8>, kFusedWG);
     const int gi_full = h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ;
     const int gc_full = (int)B.cull_grid_fused();
+    // texels (Base::texel_for; z-half waves only) for the batches this call prepares
+    const bool tex = h->nz == 4 && B.texel_for(dk, B.n_bricks);
+    struct TexelScope {
+        Base& b;
+        ~TexelScope() { b.texel_now = false; }
+    } tex_scope{B};
+    B.texel_now = tex;
     Batch bts[kSets];
     for (int L = -2; L < nb; ++L) {
         const int jp = L + 2;  // batch prepped by this launch
@@ -160,7 +167,8 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
         if (has_i) TSDF_TRY(B.prof.begin(B.stream, &e0));
         // (u32 colour registers where the volume is canonical: obs_weight 1 and NZ = 4, tsdf_device.h)
         const bool cu = TSDF_COLOR_U32 && ow1 && h->nz == 4 && B.vol.canon;
-        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0) | (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (cu ? 8 : 0);
+        const int sel = (ow1 ? 1 : 0) | (h->nz == 4 ? 2 : 0) | (dk == TSDF_DEPTH_U16_MM ? 0 : 4) | (cu ? 8 : 0) |
+                        (tex ? 16 : 0);
         const FusedArgs args{B.vol, bi, bc, bp, B.pool, B.stats, sg};
         switch (sel) {
 #define TSDF_LAUNCH(S, OW_, NZ_, DK_)                                                                   \
@@ -181,6 +189,9 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
             TSDF_LAUNCH(7, true, 4, 1)
             TSDF_LAUNCH_CU(11, true, 4, 0)
             TSDF_LAUNCH_CU(15, true, 4, 1)
+            TSDF_LAUNCH(18, false, 4, 2)
+            TSDF_LAUNCH(19, true, 4, 2)
+            TSDF_LAUNCH_CU(27, true, 4, 2)
 #undef TSDF_LAUNCH
 #undef TSDF_LAUNCH_CU
         }

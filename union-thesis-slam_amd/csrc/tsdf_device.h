@@ -142,6 +142,7 @@ struct Batch {
     Frame f[kMaxBatch];
     PyrGeo pg;
     int n;
+    int texel;  // the frames' rgbx buffers hold 8-byte depth + colour texels (DK == 2 kernels)
 };
 
 // A culled brick for the integrate: brick index (low 32 bits) | frames that kept it << 32.
@@ -465,6 +466,14 @@ __device__ unsigned buf_ld_u32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset
 __device__ double buf_ld_f64(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
                              int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.f64");
 constexpr int kBufDword3 = 0x00020000;  // gfx9 untyped buffer access
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ u32x2 buf_ld_v2u32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset,
+                              int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v2i32");
+// DK == 2 ("texels"): u16 millimetre depth + RGB8 gathered as ONE 8-byte texel per pixel (depth,
+// r | g<<8 | b<<16), which the fused launch's prep writes into the frame's rgbx buffer (Batch::texel)
+// -- one gather per voxel-step instead of two (round 6: dense -4.7 % per launch; the prep's 8 B per
+// pixel then costs more than it saves on quarter and smaller shards, so the host picks it by the
+// handle's share of the volume, Base::texel_for)
 struct FrameBufs {
     __amdgpu_buffer_rsrc_t depth, color;
 };
@@ -472,6 +481,11 @@ template <int DK, int CK>
 __device__ inline FrameBufs frame_bufs(const Frame& fr) {
     const int n = fr.W * fr.H;
     FrameBufs b;
+    if (DK == 2) {
+        static_assert(DK != 2 || CK == 0, "texels: RGB8 colour");
+        b.depth = b.color = __builtin_amdgcn_make_buffer_rsrc((void*)fr.rgbx, 8, n, kBufDword3);
+        return b;
+    }
     b.depth = __builtin_amdgcn_make_buffer_rsrc((void*)fr.depth, DK == 0 ? 2 : 8, n, kBufDword3);
     // RGB8 (CK == 0): a 4-byte load at pixel p of a 3-byte-stride structured buffer returns r, g, b in
     // bytes 0-2 (the integrate decodes those three; the range check is on the pixel index), so the
@@ -485,11 +499,11 @@ __device__ inline FrameBufs frame_bufs(const Frame& fr) {
 }
 template <int DK>
 __device__ inline unsigned depth_raw(const FrameBufs& fb, unsigned p) {
-    return DK == 0 ? (unsigned)buf_ld_u16(fb.depth, (int)p, 0, 0, 0) : 0u;
+    return DK == 0 ? (unsigned)buf_ld_u16(fb.depth, (int)p, 0, 0, 0) : 0u;  // (DK 2: the texel's)
 }
 template <int DK>
 __device__ inline double depth_m(const FrameBufs& fb, unsigned p, unsigned raw) {
-    if (DK == 0) {  // two-term 1/1000 = C_HI + C_LO: exact for every u16 (tools/check_depth_conversion.c)
+    if (DK != 1) {  // two-term 1/1000 = C_HI + C_LO: exact for every u16 (tools/check_depth_conversion.c)
         const double m = (double)raw;
         return fma(m, 0.001, m * -2.0858186326137145e-20);
     }
@@ -692,8 +706,14 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     unsigned draw[NZ];
 #pragma unroll
     for (int k = 0; k < NZ; ++k) {
-        draw[k] = depth_raw<DK>(fb, pix[k]);
-        cpx[k] = buf_ld_u32(fb.color, (int)pix[k], 0, 0, 0);
+        if (DK == 2) {
+            const u32x2 t = buf_ld_v2u32(fb.depth, (int)pix[k], 0, 0, 0);
+            draw[k] = t.x;
+            cpx[k] = t.y;
+        } else {
+            draw[k] = depth_raw<DK>(fb, pix[k]);
+            cpx[k] = buf_ld_u32(fb.color, (int)pix[k], 0, 0, 0);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
     double dep[NZ];
@@ -704,7 +724,7 @@ __device__ __forceinline__ void project_part(double trunc, const Frame& fr, doub
     for (int k = 0; k < NZ; ++k) {
         diff[k] = dep[k] - zc[k];
         // u16: RN(m / 1000) > 0 iff m > 0
-        const unsigned long long dpos = DK == 0 ? icmp32_mask(draw[k], 0u, kCmpNE) : fcmp64_mask(dep[k], 0.0, kCmpOGT);
+        const unsigned long long dpos = DK != 1 ? icmp32_mask(draw[k], 0u, kCmpNE) : fcmp64_mask(dep[k], 0.0, kCmpOGT);
         okm[k] = cand[k] & dpos & fcmp64_mask(diff[k], -trunc, kCmpOGE);
     }
 }
@@ -1650,13 +1670,14 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
             const int y = y0 + dy;
             if (y >= fr.H) continue;
             const size_t p = (size_t)y * fr.W + x0;
+            uint2 dd = make_uint2(0u, 0u);  // (u16: the 4 pixels' depth, masked)
             if (DK == 1) {  // f64 metres (the reference's own depth_im)
                 const double2 d0 = *(const double2*)((const double*)fr.depth_src + p);
                 const double2 d1 = *(const double2*)((const double*)fr.depth_src + p + 2);
                 ma = fmaxf(ma, fmaxf((float)d0.x, (float)d0.y));
                 mb = fmaxf(mb, fmaxf((float)d1.x, (float)d1.y));
             } else {
-                uint2 dd = *(const uint2*)((const unsigned short*)fr.depth_src + p);
+                dd = *(const uint2*)((const unsigned short*)fr.depth_src + p);
                 if (fr.depth_mask) {  // the demos' depth_im[depth_im == 65.535] = 0
                     unsigned lo0 = dd.x & 0xFFFFu, hi0 = dd.x >> 16, lo1 = dd.y & 0xFFFFu, hi1 = dd.y >> 16;
                     lo0 = lo0 == 65535u ? 0u : lo0;
@@ -1672,8 +1693,15 @@ __device__ inline void prep_vec_tile(const Batch& bt, unsigned int* count, int t
             if (fr.rgbx) {  // (frames the integrate cannot gather in place, frame_bufs)
                 const unsigned* q = (const unsigned*)((const unsigned char*)fr.color + 3 * p);
                 const unsigned a = q[0], b = q[1], cc = q[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
-                *(uint4*)((unsigned*)fr.rgbx + p) =
-                    make_uint4(a & 0xFFFFFFu, (a >> 24) | ((b & 0xFFFFu) << 8), (b >> 16) | ((cc & 0xFFu) << 16), cc >> 8);
+                const uint4 c4 = make_uint4(a & 0xFFFFFFu, (a >> 24) | ((b & 0xFFFFu) << 8),
+                                            (b >> 16) | ((cc & 0xFFu) << 16), cc >> 8);
+                if (DK == 2) {  // 8-byte texels (depth, colour)
+                    uint4* t = (uint4*)((uint2*)fr.rgbx + p);
+                    t[0] = make_uint4(dd.x & 0xFFFFu, c4.x, dd.x >> 16, c4.y);
+                    t[1] = make_uint4(dd.y & 0xFFFFu, c4.z, dd.y >> 16, c4.w);
+                } else {
+                    *(uint4*)((unsigned*)fr.rgbx + p) = c4;
+                }
             }
         }
     }
@@ -1755,7 +1783,8 @@ __global__ __launch_bounds__(1024) void k_prep(Batch bt, unsigned int* count) {
                 }
                 if (CK == 0 && rgbx) {
                     const unsigned char* q = (const unsigned char*)fr.color + 3 * (size_t)p;
-                    rgbx[p] = (unsigned)q[0] | ((unsigned)q[1] << 8) | ((unsigned)q[2] << 16);
+                    const unsigned c = (unsigned)q[0] | ((unsigned)q[1] << 8) | ((unsigned)q[2] << 16);
+                    rgbx[p] = c;
                 }
                 m1 = fmaxf(m1, (float)d);
             }

@@ -931,7 +931,8 @@ void launch_integrate(tsdf_hash* h, const Batch& bt, int dk, int ck, const ListE
                       unsigned int* count, int n_list) {
     Base& B = h->b;
     const unsigned grid = B.grid_for((const void*)k_integrate<true, 0, 0, true>);
-    const int sel = (dk == TSDF_DEPTH_U16_MM ? 0 : 2) | (ck == TSDF_COLOR_RGB8 ? 0 : 1);
+    // (a batch of the fused path may carry texels: its re-run gathers them too)
+    const int sel = bt.texel ? 4 : (dk == TSDF_DEPTH_U16_MM ? 0 : 2) | (ck == TSDF_COLOR_RGB8 ? 0 : 1);
     switch (sel) {
 #define TSDF_LAUNCH(S, DK_, CK_)                                                                        \
     case S:                                                                                             \
@@ -942,6 +943,7 @@ void launch_integrate(tsdf_hash* h, const Batch& bt, int dk, int ck, const ListE
         TSDF_LAUNCH(1, 0, 1)
         TSDF_LAUNCH(2, 1, 0)
         TSDF_LAUNCH(3, 1, 1)
+        TSDF_LAUNCH(4, 2, 0)
 #undef TSDF_LAUNCH
     }
 }
@@ -1030,6 +1032,13 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     // (a shard that owns no brick -- more shards than bricks -- still runs one cull workgroup, which
     // lists nothing, like the in-line path's max(1, ...))
     const int gc_full = h->t.owned ? std::max(1, (h->t.n_owned + 63) / 64) : (int)B.cull_grid_fused();
+    // texels (Base::texel_for) by the bricks this handle owns
+    const bool tex = B.texel_for(dk, h->t.owned ? (long long)h->t.n_owned : B.n_bricks);
+    struct TexelScope {
+        Base& b;
+        ~TexelScope() { b.texel_now = false; }
+    } tex_scope{B};
+    B.texel_now = tex;
     Batch bts[kSets];
     h->set_rot = (rot + nb) % kSets;
     for (int L = -2; L < nb; ++L) {
@@ -1088,7 +1097,10 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
         TSDF_HOST_TIME(3);
         // (u32 colour registers where the table's blocks are canonical, tsdf_device.h)
         const bool cu = TSDF_COLOR_U32 && B.vol.canon;
-        if (dk == TSDF_DEPTH_U16_MM) {
+        if (tex) {
+            if (cu) hipLaunchKernelGGL((k_fused_hash<2, true>), dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+            else hipLaunchKernelGGL(k_fused_hash<2>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
+        } else if (dk == TSDF_DEPTH_U16_MM) {
             if (cu) hipLaunchKernelGGL((k_fused_hash<0, true>), dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
             else hipLaunchKernelGGL(k_fused_hash<0>, dim3((unsigned)grid), dim3(kFusedHashWG), 0, B.stream, args);
         } else {

@@ -82,6 +82,18 @@ struct Base {
     // RGB8 frames gathered in place by the integrate (frame_bufs) where the byte after a frame is
     // readable, instead of through the prep's RGBX copy (TSDF_RGB_DIRECT=0: always the copy)
     bool rgb_direct = true;
+    // Texels (DK == 2 kernels, tsdf_device.h): the fused launches of u16 + RGB8 frames gather one
+    // 8-byte (depth, colour) texel per voxel-step, written by their prep, where the handle holds at
+    // least kTexelMinBricks of the volume's bricks -- the integrate's gathers then outweigh the
+    // prep's 8 B per pixel (round 6: whole 512^3 volume -4.7 % per launch, eighth shard +4.7 %).
+    // TSDF_TEXEL=0 / 1 forces it off / on.  texel_now: the batches being prepared carry texels.
+    int texel_mode = -1;  // (-1: by the rule)
+    bool texel_now = false;
+    static constexpr long long kTexelMinBricks = 1ll << 17;
+    bool texel_for(int dk, long long owned_bricks) const {
+        if (dk != TSDF_DEPTH_U16_MM) return false;
+        return texel_mode >= 0 ? texel_mode != 0 : owned_bricks >= kTexelMinBricks;
+    }
     // deferred f64-metre frames that are all RN(k / 1000) staged as u16 millimetres (defer_push;
     // TSDF_DEFER_MM=0: as they come)
     bool defer_mm = true;
