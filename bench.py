@@ -54,7 +54,21 @@ PMC_PROFILE = os.path.join(REPO, "profiles", "pmc_integrate_r06.json")
 SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r06.json")
 HASH_WORKLOAD = ("config[2]: the same frames into a voxel hash over the 512^3 @ 2 cm extent (8^3 blocks, 2^22 "
                  "slots, pool grown from 2^15 blocks)")
-HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r06.json")  # traffic + SQ of k_fused_hash<0, true>
+HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r06.json")  # traffic + SQ of k_fused_hash<DK, true>
+TEXEL_MIN_BRICKS = 3 << 15  # Base::kTexelMinBricks (tsdf_host.h)
+
+
+def texel_dk(bricks):
+    """The integrate variant the library picks for a handle of `bricks` bricks (Base::texel_for):
+    2 = one 8-byte depth + colour texel gather per voxel-step, 0 = a depth and a colour gather."""
+    env = os.environ.get("TSDF_TEXEL")
+    on = (int(env) != 0) if env is not None else bricks >= TEXEL_MIN_BRICKS
+    return 2 if on else 0
+
+
+def hash_owned_bricks(n):
+    """Bricks a bucket-range hash shard of the bench's extent owns, about 1/n of them."""
+    return (int(round(ROOM / VOXEL)) // 8) ** 3 // max(1, n)
 # config[2]'s load-factor sweep (tools/hash_sweep.py), quoted only for the library build it measured
 HASH_SWEEP = os.path.join(REPO, "profiles", "r06_hash_sweep.json")
 
@@ -465,8 +479,9 @@ def main():
     vox = sum_over_ranks(float(st["voxel_updates"]))
     fps = Kf / dt_max
     kernel_s = st["kernel_ms"] / 1e3
-    roof = integrate_roofline(st, Kf, "tsdf::k_fused<true, 4, 0, true>: integrates batch k (and culls k+1, preps k+2 in "
-                                      "the same launch)", first_timed)
+    local_bricks = int(np.prod((np.asarray(vol._local_dim) + 7) // 8))
+    roof = integrate_roofline(st, Kf, f"tsdf::k_fused<true, 4, {texel_dk(local_bricks)}, true>: integrates batch k "
+                                      "(and culls k+1, preps k+2 in the same launch)", first_timed)
     if roof is not None:
         attach_profiles(roof, st, _ffi.build_id(), PMC_PROFILE, SQ_PROFILE, WORKLOAD)
     vf_mean = st["voxel_updates"] / Kf
@@ -610,7 +625,8 @@ def main():
                                         "pool_capacity_in_run: before it, with the growth headroom of the "
                                         "launches in flight); dense: three f32 arrays of the volume",
                     "roofline": None}
-        hroof = integrate_roofline(hs, Kf, "tsdf::k_fused_hash<0, true>: integrates batch k (find-or-insert of its "
+        hroof = integrate_roofline(hs, Kf, f"tsdf::k_fused_hash<{texel_dk(hash_owned_bricks(n))}, true>: integrates "
+                                           "batch k (find-or-insert of its "
                                            "blocks), culls k+1 and preps k+2 in the same launch; the window "
                                            "inserts blocks_allocated_in_window blocks",
                                    blocks_touched=hs["lookups"])

@@ -35,8 +35,22 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "tsdf::k_fused<true, 4, 0, true>"  # (CU = true: u32 colour registers, the canonical volume)
+# the bench's integrate launches (CU = true: u32 colour registers, the canonical volume); DK = 2 is
+# the texel variant the host picks for handles of >= 2^17 bricks (Base::texel_for), DK = 0 the
+# two-gather one (older builds, TSDF_TEXEL=0).  use_kernels() picks the one a profile holds.
+KERNELS = ("tsdf::k_fused<true, 4, 2, true>", "tsdf::k_fused<true, 4, 0, true>")
+HASH_KERNELS = ("k_fused_hash<2, true>", "k_fused_hash<0, true>")
+KERNEL, HASH_KERNEL = KERNELS[0], HASH_KERNELS[0]
 W, K = 5, 20  # the driver's --warmup / --steps
+
+
+def use_kernels(csv_path):
+    """Set KERNEL / HASH_KERNEL to the variants the profile's rows name (texel variant first)."""
+    global KERNEL, HASH_KERNEL
+    with open(csv_path) as f:
+        text = f.read()
+    KERNEL = next((k for k in KERNELS if k in text), KERNELS[0])
+    HASH_KERNEL = next((k for k in HASH_KERNELS if k in text), HASH_KERNELS[0])
 
 
 def bench_line(path):
@@ -66,6 +80,7 @@ def timed(rows_by_dispatch, first):
 def pmc_timed(path, counter, first, ids=None):
     """The counter's values on the K timed launches (summed over dimensions / XCDs); ids: take
     exactly these dispatches (the timed set found on another counter of the same pass)."""
+    use_kernels(path)
     per = {}
     for row in csv.DictReader(open(path)):
         if row["Counter_Name"] != counter or KERNEL not in row["Kernel_Name"]:
@@ -110,6 +125,7 @@ def main(tag):
     src = os.path.join(REPO, "gpurun_out", "profile")
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
+    use_kernels(os.path.join(src, "kernel_trace_tsdf.csv"))
     shutil.copy(os.path.join(src, "kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     line = bench_line(os.path.join(src, "bench_under_rocprof.json"))
     with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
@@ -161,6 +177,7 @@ def sq(tag):
     """gpurun_out/pmc_sq/pmc_sq.csv (tools/gpu/run_pmc_sq.sh) -> profiles/pmc_sq_<tag>.json: SQ
     counters per timed launch of the dense integrate launch and its VALU-busy fraction."""
     src = os.path.join(REPO, "gpurun_out", "pmc_sq")
+    use_kernels(os.path.join(src, "pmc_sq.csv"))
     names = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
              "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
     pl = bench_line(os.path.join(src, "bench.json"))
@@ -189,15 +206,15 @@ def sq(tag):
     print(json.dumps(out, indent=1))
 
 
-HASH_KERNEL = "k_fused_hash<0, true>"
 SQ_NAMES = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
             "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
 
 
 def hash_windows(path):
-    """Per-dispatch counters of k_fused_hash<0, true> in one pass -> (inserting window, repeat window):
+    """Per-dispatch counters of HASH_KERNEL in one pass -> (inserting window, repeat window):
     the hash leg ends with the timed call (K + 2 launches: two pipeline fills, then K integrating)
     and the no-allocation repeat (K + 2 more), the process's last 2 (K + 2) launches of the kernel."""
+    use_kernels(path)
     per = {}
     for r in csv.DictReader(open(path)):
         if HASH_KERNEL not in r["Kernel_Name"]:
@@ -213,6 +230,7 @@ def hash_windows(path):
 def hash_profile(tag):
     """profile/pmc_{FETCH,WRITE}_SIZE.csv and pmc_sq/pmc_sq.csv -> profiles/pmc_hash_<tag>.json."""
     src = os.path.join(REPO, "gpurun_out", "profile")
+    use_kernels(os.path.join(src, "pmc_FETCH_SIZE.csv"))
     sys.path.insert(0, REPO)
     import bench
     out = {"kernel": "tsdf::" + HASH_KERNEL, "workload": bench.HASH_WORKLOAD,

@@ -472,8 +472,8 @@ __device__ u32x2 buf_ld_v2u32(__amdgpu_buffer_rsrc_t r, int vindex, int voffset,
 // DK == 2 ("texels"): u16 millimetre depth + RGB8 gathered as ONE 8-byte texel per pixel (depth,
 // r | g<<8 | b<<16), which the fused launch's prep writes into the frame's rgbx buffer (Batch::texel)
 // -- one gather per voxel-step instead of two (round 6: dense -4.7 % per launch; the prep's 8 B per
-// pixel then costs more than it saves on quarter and smaller shards, so the host picks it by the
-// handle's share of the volume, Base::texel_for)
+// pixel then costs more than it saves on eighth shards, so the host picks it by the handle's
+// bricks, Base::texel_for)
 struct FrameBufs {
     __amdgpu_buffer_rsrc_t depth, color;
 };

@@ -89,7 +89,7 @@ struct Base {
     // TSDF_TEXEL=0 / 1 forces it off / on.  texel_now: the batches being prepared carry texels.
     int texel_mode = -1;  // (-1: by the rule)
     bool texel_now = false;
-    static constexpr long long kTexelMinBricks = 1ll << 17;
+    static constexpr long long kTexelMinBricks = 3ll << 15;  // (between a half and a quarter of 512^3 @ 8^3)
     bool texel_for(int dk, long long owned_bricks) const {
         if (dk != TSDF_DEPTH_U16_MM) return false;
         return texel_mode >= 0 ? texel_mode != 0 : owned_bricks >= kTexelMinBricks;
