@@ -55,14 +55,14 @@ SQ_PROFILE = os.path.join(REPO, "profiles", "pmc_sq_r06.json")
 HASH_WORKLOAD = ("config[2]: the same frames into a voxel hash over the 512^3 @ 2 cm extent (8^3 blocks, 2^22 "
                  "slots, pool grown from 2^15 blocks)")
 HASH_PROFILE = os.path.join(REPO, "profiles", "pmc_hash_r06.json")  # traffic + SQ of k_fused_hash<DK, true>
-TEXEL_MIN_BRICKS = 3 << 15  # Base::kTexelMinBricks (tsdf_host.h)
+TEXEL_MIN_BRICKS = {"dense": 3 << 14, "hash": 3 << 15}  # Base::kTexelMinBricks* (tsdf_host.h)
 
 
-def texel_dk(bricks):
+def texel_dk(bricks, kind="dense"):
     """The integrate variant the library picks for a handle of `bricks` bricks (Base::texel_for):
     2 = one 8-byte depth + colour texel gather per voxel-step, 0 = a depth and a colour gather."""
     env = os.environ.get("TSDF_TEXEL")
-    on = (int(env) != 0) if env is not None else bricks >= TEXEL_MIN_BRICKS
+    on = (int(env) != 0) if env is not None else bricks >= TEXEL_MIN_BRICKS[kind]
     return 2 if on else 0
 
 
@@ -625,7 +625,7 @@ def main():
                                         "pool_capacity_in_run: before it, with the growth headroom of the "
                                         "launches in flight); dense: three f32 arrays of the volume",
                     "roofline": None}
-        hroof = integrate_roofline(hs, Kf, f"tsdf::k_fused_hash<{texel_dk(hash_owned_bricks(n))}, true>: integrates "
+        hroof = integrate_roofline(hs, Kf, f"tsdf::k_fused_hash<{texel_dk(hash_owned_bricks(n), 'hash')}, true>: integrates "
                                            "batch k (find-or-insert of its "
                                            "blocks), culls k+1 and preps k+2 in the same launch; the window "
                                            "inserts blocks_allocated_in_window blocks",

@@ -17,6 +17,7 @@
 #   py:<script>[:args] python tools/gpu/<script> [args, '+'-separated]
 #   pylib:<lib>:<script>[:args]  the same with TSDF_HIP_LIB=abtest/lib<lib>.so
 #   tool:<script>[:args]:<tag>  python tools/<script> [args], output to <dir>/<tag>.out
+#   toolenv:<VAR=VAL[+..]>:<script>:<args>:<tag>  the same with that environment
 #   bin:<path>         a prebuilt probe binary (tools/gpu/<name>), output to <dir>/<name>.out
 #   kt:<script>[:args] the same under rocprofv3 --kernel-trace --stats (stats csv copied to <dir>)
 #   pmcbin:<binary>:<c1+c2..>[:<c1+..>]  rocprofv3 --pmc passes over a prebuilt probe (csv to <dir>)
@@ -108,6 +109,11 @@ for step in "$@"; do
     tool:*)
       IFS=: read -r _ script args tag <<< "$step"
       timeout -k 10 900 python -u "tools/$script" ${args//+/ } > "$O/$tag.out" 2> "$O/$tag.err" || exit 1
+      ;;
+    toolenv:*)  # toolenv:VAR=VAL[+VAR2=VAL2]:<script>:<args>:<tag> -- tool: with that environment
+      IFS=: read -r _ envspec script args tag <<< "$step"
+      IFS='+' read -ra envs <<< "$envspec"
+      env "${envs[@]}" timeout -k 10 900 python -u "tools/$script" ${args//+/ } > "$O/$tag.out" 2> "$O/$tag.err" || exit 1
       ;;
     bin:*)
       b=${step#bin:}

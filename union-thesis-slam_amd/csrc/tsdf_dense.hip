@@ -123,7 +123,7 @@ int dense_run_fused(tsdf_dense* h, int n_frames, const void* depth, int dk, cons
     const int gi_full = h->gi_per_cu ? std::min(gi_occ, h->gi_per_cu * B.n_cu) : gi_occ;
     const int gc_full = (int)B.cull_grid_fused();
     // texels (Base::texel_for; z-half waves only) for the batches this call prepares
-    const bool tex = h->nz == 4 && B.texel_for(dk, B.n_bricks);
+    const bool tex = h->nz == 4 && B.texel_for(dk, B.n_bricks, Base::kTexelMinBricksDense);
     struct TexelScope {
         Base& b;
         ~TexelScope() { b.texel_now = false; }

@@ -1033,7 +1033,7 @@ int hash_run_fused(tsdf_hash* h, int n_frames, const void* depth, int dk, const 
     // lists nothing, like the in-line path's max(1, ...))
     const int gc_full = h->t.owned ? std::max(1, (h->t.n_owned + 63) / 64) : (int)B.cull_grid_fused();
     // texels (Base::texel_for) by the bricks this handle owns
-    const bool tex = B.texel_for(dk, h->t.owned ? (long long)h->t.n_owned : B.n_bricks);
+    const bool tex = B.texel_for(dk, h->t.owned ? (long long)h->t.n_owned : B.n_bricks, Base::kTexelMinBricksHash);
     struct TexelScope {
         Base& b;
         ~TexelScope() { b.texel_now = false; }

@@ -84,15 +84,18 @@ struct Base {
     bool rgb_direct = true;
     // Texels (DK == 2 kernels, tsdf_device.h): the fused launches of u16 + RGB8 frames gather one
     // 8-byte (depth, colour) texel per voxel-step, written by their prep, where the handle holds at
-    // least kTexelMinBricks of the volume's bricks -- the integrate's gathers then outweigh the
-    // prep's 8 B per pixel (round 6: whole 512^3 volume -4.7 % per launch, eighth shard +4.7 %).
+    // least min_bricks bricks -- the integrate's gathers then outweigh the prep's 8 B per pixel.
+    // Round 6 (profiles/r06_texel/), shards of 512^3 @ 8^3 bricks, texels against two gathers per
+    // launch (scaling_sim, one box): dense whole -5 %, half -5 %, quarter -3 %, eighth +3 %; hash
+    // whole -5 %, half -2 %, quarter +1 %, eighth +6 %.  So dense from 3 * 2^14 bricks (between an eighth and a
+    // quarter), the hash from 3 * 2^15 (between a quarter and a half).
     // TSDF_TEXEL=0 / 1 forces it off / on.  texel_now: the batches being prepared carry texels.
     int texel_mode = -1;  // (-1: by the rule)
     bool texel_now = false;
-    static constexpr long long kTexelMinBricks = 3ll << 15;  // (between a half and a quarter of 512^3 @ 8^3)
-    bool texel_for(int dk, long long owned_bricks) const {
+    static constexpr long long kTexelMinBricksDense = 3ll << 14, kTexelMinBricksHash = 3ll << 15;
+    bool texel_for(int dk, long long owned_bricks, long long min_bricks) const {
         if (dk != TSDF_DEPTH_U16_MM) return false;
-        return texel_mode >= 0 ? texel_mode != 0 : owned_bricks >= kTexelMinBricks;
+        return texel_mode >= 0 ? texel_mode != 0 : owned_bricks >= min_bricks;
     }
     // deferred f64-metre frames that are all RN(k / 1000) staged as u16 millimetres (defer_push;
     // TSDF_DEFER_MM=0: as they come)
