@@ -40,6 +40,28 @@ def summarize(buf):
             r[name] = [int(m.sum()), float(s[m].min()), float(s[m].max()), float(np.median(e[m])), float(e[m].max()),
                        float((e[m] - s[m]).mean())]
     r["items"] = float(it[role == 0].mean()) if (role == 0).any() else 0.0
+    m = role == 0
+    if m.any():  # the integrate workgroups by XCD (XCC_ID), and whether the last ones took more items
+        xcc = (buf[3][keep] >> np.uint64(32)).astype(np.int64)
+        r["xcd_end_median"] = [float(np.median(e[m & (xcc == x)])) if (m & (xcc == x)).any() else 0.0 for x in range(8)]
+        r["xcd_end_max"] = [float(e[m & (xcc == x)].max()) if (m & (xcc == x)).any() else 0.0 for x in range(8)]
+        late = m & (e >= np.quantile(e[m], 0.9))
+        r["items_late_over_mean"] = float(it[late].mean() / max(1e-9, it[m].mean()))
+        # the two integrate workgroups of a CU (XCC, SE/SH/CU bits of HW_ID): how far apart they end,
+        # and how often the later-dispatched one (higher workgroup id) ends last
+        hw = (buf[3][keep] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        wid = np.flatnonzero(keep)
+        cu = xcc * 4096 + ((hw >> 8) & 0xFF)
+        gaps, later_last = [], []
+        for c in np.unique(cu[m]):
+            sel = np.flatnonzero(m & (cu == c))
+            if len(sel) == 2:
+                a, b2 = sel[np.argsort(wid[sel])]
+                gaps.append(abs(e[b2] - e[a]))
+                later_last.append(e[b2] > e[a])
+        r["cu_pair_gap_mean"] = float(np.mean(gaps)) if gaps else 0.0
+        r["cu_pair_later_ends_last"] = float(np.mean(later_last)) if later_last else 0.0
+        r["cu_pairs"] = len(gaps)
     return r
 
 
@@ -76,6 +98,13 @@ def main():
             rows.append(summarize(buf))
         out = {"config": label, "span_us": round(float(np.mean([r["span"] for r in rows])), 2),
                "items_mean": round(float(np.mean([r["items"] for r in rows])), 1)}
+        if all("xcd_end_median" in r for r in rows):
+            out["integrate_xcd_end_median_us"] = [round(float(x), 1) for x in np.mean([r["xcd_end_median"] for r in rows], axis=0)]
+            out["integrate_xcd_end_max_us"] = [round(float(x), 1) for x in np.mean([r["xcd_end_max"] for r in rows], axis=0)]
+            out["integrate_late10_items_over_mean"] = round(float(np.mean([r["items_late_over_mean"] for r in rows])), 3)
+            out["integrate_cu_pair_gap_us"] = round(float(np.mean([r["cu_pair_gap_mean"] for r in rows])), 1)
+            out["integrate_cu_pair_later_ends_last"] = round(float(np.mean([r["cu_pair_later_ends_last"] for r in rows])), 3)
+            out["integrate_cu_pairs"] = int(np.mean([r["cu_pairs"] for r in rows]))
         for name in ("integrate", "cull", "prep"):
             vv = np.array([r[name] for r in rows if name in r])
             if len(vv):
